@@ -1,0 +1,426 @@
+// hkv_api.cpp — the C ABI (include/hkv.h) over the HIP kernels.
+//
+// One hkv_ctx per process; per device: a stream, the fixed-base G tables,
+// the per-lane Q-table scratch sized for one full-occupancy ecmult grid, and
+// growable intermediate / bitmap / record-staging buffers. hkv_verify shards
+// contiguous 64-aligned index ranges over the devices, overlaps their H2D /
+// kernels / D2H on per-device streams and joins. No exceptions cross the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/hkv.h"
+#include "hkv_internal.h"
+#include "hkv_layout.h"
+
+namespace {
+
+thread_local std::string g_last_hip;
+
+struct DevCtx {
+  int device = -1;
+  int n_cu = 0;
+  hipStream_t stream = nullptr;
+  uint32_t* gtab = nullptr;
+  uint32_t* qs = nullptr;
+  uint32_t grid_max = 0;  // ecmult blocks (qs is sized for grid_max * WG lanes)
+  uint32_t* im = nullptr;
+  size_t im_cap = 0;      // n_pad capacity
+  uint32_t* bits = nullptr;
+  size_t bits_cap = 0;    // words
+  uint8_t* recs = nullptr;
+  size_t recs_cap = 0;    // records
+  uint32_t* hbits = nullptr;  // pinned D2H staging
+  size_t hbits_cap = 0;
+  uint32_t* pool = nullptr;
+  uint32_t pool_n = 0;
+  uint64_t pool_seed = ~0ull;
+  // optional per-kernel timing (hkv_profile_*): events on the launch stream
+  bool profile = false;
+  std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
+};
+
+}  // namespace
+
+struct hkv_ctx {
+  std::vector<DevCtx> devs;
+  std::mutex mu;
+};
+struct hkv_batch {
+  hkv_ctx* ctx = nullptr;
+  uint8_t* host = nullptr;
+  size_t cap = 0;
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+  g_last_hip = std::string(what) + ": " + hipGetErrorString(e);
+  return HKV_E_HIP;
+}
+#define HKV_TRY(expr, what)                       \
+  do {                                            \
+    hipError_t e_ = (expr);                       \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
+  if (d.im_cap < n_pad) {
+    if (d.im) (void)hipFree(d.im);
+    d.im = nullptr;
+    d.im_cap = 0;
+    HKV_TRY(hipMalloc(&d.im, n_pad * hkv::IM_WORDS * sizeof(uint32_t)), "hipMalloc(intermediate)");
+    d.im_cap = n_pad;
+  }
+  const size_t words = n_pad / 32;
+  if (d.bits_cap < words) {
+    if (d.bits) (void)hipFree(d.bits);
+    d.bits = nullptr;
+    d.bits_cap = 0;
+    HKV_TRY(hipMalloc(&d.bits, words * sizeof(uint32_t)), "hipMalloc(bits)");
+    d.bits_cap = words;
+  }
+  return HKV_OK;
+}
+
+// enqueue prologue + ecmult for n records at d_records; verdict words in d.bits
+int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st) {
+  const size_t n_pad = round_up(n, hkv::WG);
+  int rc = ensure_dev_buffers(d, n_pad);
+  if (rc) return rc;
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  if (d.profile) {
+    for (auto& x : e) HKV_TRY(hipEventCreate(&x), "hipEventCreate");
+    HKV_TRY(hipEventRecord(e[0], st), "hipEventRecord");
+  }
+  HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
+  if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
+  const uint32_t blocks = (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
+  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, d.bits, st),
+          "ecmult launch");
+  if (d.profile) {
+    HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
+    d.ev.insert(d.ev.end(), e, e + 3);
+  }
+  return HKV_OK;
+}
+
+int init_device(DevCtx& d, int device) {
+  d.device = device;
+  HKV_TRY(hipSetDevice(device), "hipSetDevice");
+  hipDeviceProp_t prop;
+  HKV_TRY(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    g_last_hip = std::string("device is ") + prop.gcnArchName + ", libhkv is built for gfx950 only";
+    return HKV_E_NODEV;
+  }
+  d.n_cu = prop.multiProcessorCount;
+  HKV_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
+  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");
+  int per_cu = 0;
+  HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
+  if (per_cu < 1) per_cu = 1;
+  d.grid_max = (uint32_t)(d.n_cu * per_cu);
+  const size_t lanes = (size_t)d.grid_max * hkv::WG;
+  HKV_TRY(hipMalloc(&d.qs, lanes * hkv::QTAB_QUADS * 16), "hipMalloc(qtab scratch)");
+  HKV_TRY(hkv::launch_gtable(d.gtab, d.stream), "gtable launch");
+  HKV_TRY(hipStreamSynchronize(d.stream), "gtable sync");
+  return HKV_OK;
+}
+
+void clear_events(DevCtx& d) {
+  for (auto e : d.ev) (void)hipEventDestroy(e);
+  d.ev.clear();
+}
+
+void free_device(DevCtx& d) {
+  if (d.device < 0) return;
+  (void)hipSetDevice(d.device);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  (void)hipDeviceSynchronize();
+  clear_events(d);
+  if (d.gtab) (void)hipFree(d.gtab);
+  if (d.qs) (void)hipFree(d.qs);
+  if (d.im) (void)hipFree(d.im);
+  if (d.bits) (void)hipFree(d.bits);
+  if (d.recs) (void)hipFree(d.recs);
+  if (d.pool) (void)hipFree(d.pool);
+  if (d.hbits) (void)hipHostFree(d.hbits);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d = DevCtx();
+}
+
+int ensure_pool(DevCtx& d, uint64_t seed, uint32_t pool_n, hipStream_t st) {
+  if (d.pool && d.pool_n == pool_n && d.pool_seed == seed) return HKV_OK;
+  if (d.pool) (void)hipFree(d.pool);
+  d.pool = nullptr;
+  HKV_TRY(hipMalloc(&d.pool, (size_t)pool_n * 16 * sizeof(uint32_t)), "hipMalloc(pool)");
+  HKV_TRY(hkv::launch_gen_pool(seed, pool_n, d.pool, st), "gen pool launch");
+  d.pool_n = pool_n;
+  d.pool_seed = seed;
+  return HKV_OK;
+}
+
+// Self-check at open: 256 generated valid records must all verify.
+int self_check(DevCtx& d) {
+  const size_t n = 256;
+  uint8_t* recs = nullptr;
+  HKV_TRY(hipMalloc(&recs, n * hkv::REC_SIZE), "hipMalloc(selfcheck)");
+  int rc = ensure_pool(d, 0x484B5630ull, 16, d.stream);
+  if (!rc) {
+    hipError_t e = hkv::launch_gen_records(0x484B5630ull, (uint32_t)n, d.pool, d.pool_n, 250, recs, d.stream);
+    if (e != hipSuccess) rc = hip_fail(e, "selfcheck gen");
+  }
+  if (!rc) rc = enqueue_verify(d, recs, n, HKV_MODE_LIBSECP, d.stream);
+  uint32_t words[8] = {0};
+  if (!rc) {
+    hipError_t e = hipMemcpyAsync(words, d.bits, sizeof(words), hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+    if (e != hipSuccess) rc = hip_fail(e, "selfcheck copy");
+  }
+  (void)hipFree(recs);
+  if (rc) return rc;
+  for (uint32_t w : words)
+    if (w != 0xFFFFFFFFu) {
+      g_last_hip = "self-check: generated valid signatures did not verify";
+      return HKV_E_INTERNAL;
+    }
+  return HKV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t hkv_version(void) { return (1u << 16) | 0u; }
+
+const char* hkv_strerror(int err) {
+  switch (err) {
+    case HKV_OK: return "ok";
+    case HKV_E_ARG: return "invalid argument";
+    case HKV_E_NODEV: return "no usable gfx950 device";
+    case HKV_E_OOM: return "out of memory";
+    case HKV_E_HIP: return "HIP runtime error";
+    case HKV_E_INTERNAL: return "internal self-check failed";
+    default: return "unknown error";
+  }
+}
+const char* hkv_last_hip_error(void) { return g_last_hip.c_str(); }
+
+int hkv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int hkv_open_devices(const int* device_ids, int n_ids, uint32_t flags, hkv_ctx** out) {
+  if (!out || n_ids <= 0 || !device_ids) return HKV_E_ARG;
+  *out = nullptr;
+  hkv_ctx* ctx = new (std::nothrow) hkv_ctx();
+  if (!ctx) return HKV_E_OOM;
+  ctx->devs.resize(n_ids);
+  for (int k = 0; k < n_ids; ++k) {
+    int rc = init_device(ctx->devs[k], device_ids[k]);
+    if (!rc && !(flags & HKV_OPEN_NO_SELFCHECK)) rc = self_check(ctx->devs[k]);
+    if (rc) {
+      for (auto& d : ctx->devs) free_device(d);
+      delete ctx;
+      return rc;
+    }
+  }
+  *out = ctx;
+  return HKV_OK;
+}
+
+int hkv_open(int n_gpus, uint32_t flags, hkv_ctx** out) {
+  if (!out) return HKV_E_ARG;
+  int avail = hkv_device_count();
+  if (avail <= 0) return HKV_E_NODEV;
+  if (n_gpus <= 0 || n_gpus > avail) n_gpus = avail;
+  std::vector<int> ids(n_gpus);
+  for (int k = 0; k < n_gpus; ++k) ids[k] = k;
+  return hkv_open_devices(ids.data(), n_gpus, flags, out);
+}
+
+void hkv_close(hkv_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& d : ctx->devs) free_device(d);
+  delete ctx;
+}
+
+int hkv_ctx_num_devices(const hkv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int hkv_batch_alloc(hkv_ctx* ctx, size_t max_n, hkv_batch** out) {
+  if (!ctx || !out || max_n == 0) return HKV_E_ARG;
+  hkv_batch* b = new (std::nothrow) hkv_batch();
+  if (!b) return HKV_E_OOM;
+  if (hipHostMalloc(reinterpret_cast<void**>(&b->host), max_n * hkv::REC_SIZE, hipHostMallocPortable) !=
+      hipSuccess) {
+    delete b;
+    return HKV_E_OOM;
+  }
+  std::memset(b->host, 0, max_n * hkv::REC_SIZE);
+  b->ctx = ctx;
+  b->cap = max_n;
+  *out = b;
+  return HKV_OK;
+}
+void hkv_batch_free(hkv_batch* b) {
+  if (!b) return;
+  if (b->host) (void)hipHostFree(b->host);
+  delete b;
+}
+uint8_t* hkv_batch_records(hkv_batch* b) { return b ? b->host : nullptr; }
+size_t hkv_batch_capacity(const hkv_batch* b) { return b ? b->cap : 0; }
+
+static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_t mode, uint32_t* out) {
+  if (!ctx || !host || !out || mode > HKV_MODE_HASKOIN) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  const size_t nd = ctx->devs.size();
+  // contiguous shards, 64-aligned starts; the last shard takes the remainder
+  size_t per = round_up((n + nd - 1) / nd, 64);
+  struct Shard { size_t lo, hi; };
+  std::vector<Shard> shards;
+  for (size_t k = 0; k < nd; ++k) {
+    size_t lo = std::min(n, k * per), hi = std::min(n, lo + per);
+    shards.push_back({lo, hi});
+  }
+  for (size_t k = 0; k < nd; ++k) {
+    DevCtx& d = ctx->devs[k];
+    const size_t len = shards[k].hi - shards[k].lo;
+    if (!len) continue;
+    HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+    if (d.recs_cap < len) {
+      if (d.recs) (void)hipFree(d.recs);
+      d.recs = nullptr;
+      d.recs_cap = 0;
+      HKV_TRY(hipMalloc(&d.recs, len * hkv::REC_SIZE), "hipMalloc(records)");
+      d.recs_cap = len;
+    }
+    const size_t words = (len + 31) / 32;
+    if (d.hbits_cap < words) {
+      if (d.hbits) (void)hipHostFree(d.hbits);
+      d.hbits = nullptr;
+      d.hbits_cap = 0;
+      HKV_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.hbits), words * 4, hipHostMallocPortable),
+              "hipHostMalloc(bits)");
+      d.hbits_cap = words;
+    }
+    HKV_TRY(hipMemcpyAsync(d.recs, host + shards[k].lo * hkv::REC_SIZE, len * hkv::REC_SIZE,
+                           hipMemcpyHostToDevice, d.stream),
+            "H2D records");
+    int rc = enqueue_verify(d, d.recs, len, mode, d.stream);
+    if (rc) return rc;
+    HKV_TRY(hipMemcpyAsync(d.hbits, d.bits, words * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
+  }
+  for (size_t k = 0; k < nd; ++k) {
+    DevCtx& d = ctx->devs[k];
+    const size_t len = shards[k].hi - shards[k].lo;
+    if (!len) continue;
+    HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+    HKV_TRY(hipStreamSynchronize(d.stream), "verify sync");
+    const size_t words = (len + 31) / 32;
+    std::memcpy(out + shards[k].lo / 32, d.hbits, words * 4);
+  }
+  // clear bits past n in the last word (kernel already writes 0 for i >= n)
+  return HKV_OK;
+}
+
+int hkv_verify(hkv_ctx* ctx, hkv_batch* b, size_t n, uint32_t mode, uint32_t* verdict_bits) {
+  if (!b || n > b->cap) return HKV_E_ARG;
+  return verify_from_host(ctx, b->host, n, mode, verdict_bits);
+}
+
+int hkv_verify_host(hkv_ctx* ctx, const uint8_t* records, size_t n, uint32_t mode, uint32_t* verdict_bits) {
+  return verify_from_host(ctx, records, n, mode, verdict_bits);
+}
+
+int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, uint32_t mode, uint32_t* d_bits,
+                      void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !d_records || !d_bits || mode > HKV_MODE_HASKOIN)
+    return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (n > 0xFFFFFF00ull) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  int rc = enqueue_verify(d, d_records, n, mode, st);
+  if (rc) return rc;
+  const size_t words = (n + 31) / 32;
+  HKV_TRY(hipMemcpyAsync(d_bits, d.bits, words * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
+  return HKV_OK;
+}
+
+int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
+                           uint32_t uncompressed_permille, void* d_records, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !d_records || pool_size == 0 ||
+      uncompressed_permille > 1000 || n > 0xFFFFFF00ull)
+    return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  int rc = ensure_pool(d, seed ^ 0x706F6F6Cull, pool_size, st);
+  if (rc) return rc;
+  HKV_TRY(hkv::launch_gen_records(seed, (uint32_t)n, d.pool, d.pool_n, uncompressed_permille, d_records, st),
+          "gen records launch");
+  return HKV_OK;
+}
+
+int hkv_debug_op(hkv_ctx* ctx, int dev, uint32_t op, size_t n, const uint32_t* d_a, const uint32_t* d_b,
+                 uint32_t* d_out, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !d_a || !d_b || !d_out) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  HKV_TRY(hkv::launch_debug(op, (uint32_t)n, d_a, d_b, d_out, st), "debug launch");
+  return HKV_OK;
+}
+
+int hkv_profile_enable(hkv_ctx* ctx, int on) {
+  if (!ctx) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  for (auto& d : ctx->devs) {
+    (void)hipSetDevice(d.device);
+    (void)hipDeviceSynchronize();
+    clear_events(d);
+    d.profile = on != 0;
+  }
+  return HKV_OK;
+}
+
+int hkv_profile_read(hkv_ctx* ctx, int dev, double* prologue_ms, double* ecmult_ms, uint64_t* launches) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !prologue_ms || !ecmult_ms || !launches)
+    return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  double p = 0, m = 0;
+  for (size_t k = 0; k + 2 < d.ev.size(); k += 3) {
+    HKV_TRY(hipEventSynchronize(d.ev[k + 2]), "hipEventSynchronize");
+    float a = 0, b = 0;
+    HKV_TRY(hipEventElapsedTime(&a, d.ev[k], d.ev[k + 1]), "hipEventElapsedTime");
+    HKV_TRY(hipEventElapsedTime(&b, d.ev[k + 1], d.ev[k + 2]), "hipEventElapsedTime");
+    p += a;
+    m += b;
+  }
+  *prologue_ms = p;
+  *ecmult_ms = m;
+  *launches = d.ev.size() / 3;
+  clear_events(d);
+  return HKV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+// hkv_group.h — secp256k1 group operations (y^2 = x^3 + 7) in Jacobian
+// coordinates for gfx950, one point per lane.
+//
+// Formulas are the a = 0 Jacobian ones; they do not involve b, so they run
+// unchanged on any isomorphic curve y^2 = x^3 + 7*Z^6 — which is what lets the
+// verify kernel keep its per-signature table "affine" on an isomorphic curve
+// (hkv_kernels.hip, table build) and correct the final Z once.
+// Replaces (semantically) libsecp256k1 secp256k1_gej_double /
+// secp256k1_gej_add_ge_var / secp256k1_gej_add_zinv_var [dep; SURVEY §8(a) a3].
+#pragma once
+#include "hkv_scalar.h"
+
+namespace hkv {
+
+struct ge { fe x, y; };
+struct gej { fe x, y, z; };
+
+__constant__ static const uint32_t FE_GX[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                                               0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+__constant__ static const uint32_t FE_GY[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                                               0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+// beta: lambda*(x, y) = (beta*x, y)
+__constant__ static const uint32_t FE_BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                                                 0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+
+HKV_DEV void ge_set_g(ge& r) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { r.x.v[i] = FE_GX[i]; r.y.v[i] = FE_GY[i]; }
+}
+HKV_DEV void gej_set_ge(gej& r, const ge& a) {
+  r.x = a.x;
+  r.y = a.y;
+  fe_set_u32(r.z, 1);
+}
+HKV_DEV void gej_cmov(gej& r, const gej& a, bool f) {
+  fe_cmov(r.x, a.x, f);
+  fe_cmov(r.y, a.y, f);
+  fe_cmov(r.z, a.z, f);
+}
+
+// r = 2a (dbl-2009-l, 2M + 5S). a must not be the point at infinity; y != 0
+// always holds on secp256k1 (no 2-torsion). r may alias a.
+HKV_DEV void gej_double(gej& r, const gej& a) {
+  fe A, B, C, D, E, t;
+  fe_sqr(A, a.x);
+  fe_sqr(B, a.y);
+  fe_sqr(C, B);
+  fe_add(t, a.x, B);
+  fe_sqr(t, t);
+  fe_sub(t, t, A);
+  fe_sub(t, t, C);
+  fe_add(D, t, t);          // D = 2((X+B)^2 - A - C)
+  fe_mul_small(E, A, 3);    // E = 3A
+  fe_mul(r.z, a.y, a.z);
+  fe_add(r.z, r.z, r.z);    // Z3 = 2YZ
+  fe_sqr(t, E);             // F = E^2
+  fe_sub(t, t, D);
+  fe_sub(r.x, t, D);        // X3 = F - 2D
+  fe_sub(t, D, r.x);
+  fe_mul(t, E, t);
+  fe_mul_small(C, C, 8);
+  fe_sub(r.y, t, C);        // Y3 = E(D - X3) - 8C
+}
+
+// Mixed addition r = a + (bx, by) where (bx, by) is affine on the curve whose
+// Jacobian z-scale is `az` (az = a.z for a plain mixed add; az = a.z * Zg for
+// the "zinv" form that adds a point of the base curve to an accumulator that
+// lives on the isomorphic curve of scale Zg). 8M + 3S.
+// Outputs hz = (H == 0), rz = (R == 0); when hz the result is garbage and the
+// caller must substitute 2a (rz) or infinity (!rz). Writes the z-ratio H.
+HKV_DEV void gej_add_ge_core(gej& r, const gej& a, const fe& az, const fe& bx, const fe& by,
+                             bool& hz, bool& rz, fe* zr) {
+  fe z2, u2, s2, h, rr, t, hh, hhh, v;
+  fe_sqr(z2, az);
+  fe_mul(u2, bx, z2);
+  fe_mul(t, az, z2);
+  fe_mul(s2, by, t);
+  fe_sub(h, u2, a.x);
+  fe_sub(rr, s2, a.y);
+  hz = fe_is_zero(h);
+  rz = fe_is_zero(rr);
+  fe_sqr(hh, h);
+  fe_mul(hhh, h, hh);
+  fe_mul(v, a.x, hh);
+  fe_mul(r.z, a.z, h);
+  if (zr) *zr = h;
+  fe_sqr(t, rr);
+  fe_sub(t, t, hhh);
+  fe_sub(t, t, v);
+  fe_sub(t, t, v);          // X3 = R^2 - H^3 - 2V
+  fe_sub(v, v, t);
+  fe_mul(v, rr, v);
+  fe_mul(hhh, a.y, hhh);
+  fe_sub(r.y, v, hhh);      // Y3 = R(V - X3) - Y1 H^3
+  r.x = t;
+}
+
+// Complete "accumulate" step used by every ecmult loop:
+//   acc (+inf flag) += T  where T = (tx, ty) affine (scale az as above),
+//   `take` = this lane adds (digit != 0). Handles acc = inf, acc = T (double),
+//   acc = -T (infinity) exactly. inf_init = (tx, ty, 1) is what acc becomes
+//   when it was infinity (caller supplies it already mapped to acc's curve).
+HKV_DEV void gej_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, const fe& ty,
+                            const fe& itx, const fe& ity, bool take) {
+  gej s;
+  bool hz, rz;
+  gej_add_ge_core(s, acc, az, tx, ty, hz, rz, nullptr);
+  const bool degenerate = take && !inf && hz;
+  if (__builtin_expect(__any(degenerate), 0)) {
+    gej d;
+    gej_double(d, acc);
+    gej_cmov(s, d, rz);
+  }
+  // new state
+  const bool to_inf = take && !inf && hz && !rz;
+  const bool from_inf = take && inf;
+  gej_cmov(acc, s, take && !inf && !(hz && !rz));
+  if (from_inf) {
+    acc.x = itx;
+    acc.y = ity;
+    fe_set_u32(acc.z, 1);
+  }
+  inf = (inf && !take) || to_inf;
+}
+
+}  // namespace hkv

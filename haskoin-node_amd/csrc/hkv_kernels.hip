@@ -1,0 +1,635 @@
+// hkv_kernels.hip — batch secp256k1 ECDSA verify kernels for gfx950.
+//
+// Pipeline per batch (one lane per signature, no MFMA: 256-bit integer work):
+//   1. hkv_prologue_kernel  — record parse (compact sig + SEC1 pubkey incl.
+//      hybrid keys and sqrt decompression), high-S policy, m = msg mod n,
+//      s^-1, u1 = m/s, u2 = r/s, GLV split of u2. Writes a SoA intermediate.
+//   2. hkv_ecmult_kernel    — per-lane table of 1..8 * Q on an isomorphic
+//      curve (one common Z, so all Q additions are mixed), then a shared
+//      doubling chain of 132 bits with radix-16 Booth digits for k1*Q and
+//      k2*(lambda Q) and radix-256 Booth digits for u1_lo*G and
+//      u1_hi*(2^128 G) (G tables staged in LDS), then the inversion-free
+//      Jacobian x compare (r*Z^2 == X, and (r+n)*Z^2 == X when r < p-n).
+//      Verdicts leave as a ballot bitmap, one 64-bit word per wave.
+//   3. hkv_gtable_kernel    — once per context: the two fixed-base tables.
+//   4. hkv_gen_*            — synthetic valid batches (keyless construction,
+//      SURVEY.md §8(c)) for the benchmark and the tests.
+//
+// Reference semantics restated: libsecp256k1 secp256k1_ec_pubkey_parse,
+// secp256k1_ecdsa_signature_parse_compact, secp256k1_ecdsa_signature_normalize,
+// secp256k1_ecdsa_verify, and haskoin-core verifyHashSig (normalize first)
+// [dep; pinned /root/reference/stack.yaml:8-10; SURVEY.md §8(a) a1, a3-a6].
+#include "hkv_group.h"
+#include "hkv_layout.h"
+#include "hkv_internal.h"
+
+namespace hkv {
+
+// ---------------------------------------------------------------------------
+// record access
+// ---------------------------------------------------------------------------
+// little-endian 32-bit word at byte offset `off` of the record (off compile-time)
+HKV_DEV uint32_t rec_word_at(const uint32_t* w, int off) {
+  const int k = off >> 2, s = off & 3;
+  if (s == 0) return w[k];
+  return __builtin_amdgcn_alignbyte(w[k + 1], w[k], s);
+}
+// 32 big-endian bytes at byte offset `off` -> 8 limbs (limb 0 least significant)
+HKV_DEV void rec_be256(uint32_t out[8], const uint32_t* w, int off) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[7 - j] = __builtin_bswap32(rec_word_at(w, off + 4 * j));
+}
+
+// p - n: r + n < p  <=>  r < p - n
+__constant__ static const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u, 1u, 0, 0, 0};
+
+// ---------------------------------------------------------------------------
+// 1. prologue
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(WG) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
+                                                          uint32_t n_pad, uint32_t mode,
+                                                          uint32_t* __restrict__ im) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  uint32_t w[REC_WORDS];
+  if (i < n) {
+    const uint2* src = reinterpret_cast<const uint2*>(recs + (size_t)i * REC_WORDS);
+#pragma unroll
+    for (int k = 0; k < REC_WORDS / 2; ++k) {
+      uint2 v = src[k];
+      w[2 * k] = v.x;
+      w[2 * k + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < REC_WORDS; ++k) w[k] = 0;
+  }
+
+  // --- signature: compact parse (overflow -> fail), normalize / high-S policy
+  sc r, s, m;
+  rec_be256(r.v, w, 32);
+  rec_be256(s.v, w, 64);
+  rec_be256(m.v, w, 0);
+  bool ok = (i < n) && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
+  const bool high = sc_is_high(s);
+  if (mode == HKV_MODE_HASKOIN) {
+    sc ns;
+    sc_neg(ns, s);
+    if (high) s = ns;  // secp256k1_ecdsa_signature_normalize
+  } else {
+    ok = ok && !high;  // secp256k1_ecdsa_verify rejects high-S
+  }
+  ok = ok && !u256_is_zero(r.v) && !u256_is_zero(s.v);
+  sc_cond_sub_n(m.v);  // m = msg32 mod n (msg32 < 2^256 < 2n)
+
+  // --- pubkey: secp256k1_ec_pubkey_parse
+  const uint32_t pklen = w[24] & 0xFFu;
+  const uint32_t prefix = (w[24] >> 8) & 0xFFu;
+  const bool comp = (pklen == 33u) && (prefix == 2u || prefix == 3u);
+  const bool unc = (pklen == 65u) && (prefix == 4u || prefix == 6u || prefix == 7u);
+  fe x, y, rhs, t;
+  rec_be256(x.v, w, 98);
+  rec_be256(y.v, w, 130);
+  bool pk_ok = (comp || unc) && u256_lt_p(x.v);
+  if (unc) pk_ok = pk_ok && u256_lt_p(y.v);
+  fe_sqr(t, x);
+  fe_mul(t, t, x);
+  fe seven;
+  fe_set_u32(seven, 7);
+  fe_add(rhs, t, seven);
+  if (__any(comp)) {
+    fe yc, y2;
+    fe_sqrt_cand(yc, rhs);
+    fe_sqr(y2, yc);
+    const bool is_sq = fe_equal(y2, rhs);
+    fe_normalize(yc);
+    fe ny;
+    fe_neg(ny, yc);
+    fe_normalize(ny);
+    const bool flip = (yc.v[0] & 1u) != (prefix & 1u);
+    if (comp) {
+      pk_ok = pk_ok && is_sq;
+      y = flip ? ny : yc;
+    }
+  }
+  if (unc) {
+    fe y2;
+    fe_sqr(y2, y);
+    pk_ok = pk_ok && fe_equal(y2, rhs);
+    if (prefix != 4u) pk_ok = pk_ok && ((y.v[0] & 1u) == (prefix & 1u));  // hybrid parity
+  }
+  ok = ok && pk_ok;
+
+  // --- scalars: s^-1, u1, u2, GLV split of u2
+  sc sinv, u1, u2;
+  sc_inv(sinv, s);
+  sc_mul(u1, m, sinv);
+  sc_mul(u2, r, sinv);
+  uint32_t k1[5], k2[5];
+  bool n1, n2;
+  const bool glv_ok = glv_split(u2, k1, n1, k2, n2);
+
+  uint32_t flags = (ok ? FLAG_VALID : 0u) | (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) |
+                   (glv_ok ? 0u : FLAG_GLV_OVF);
+  if (!glv_ok) flags &= ~FLAG_VALID;  // unreachable for a correct basis; fail closed
+  im[(size_t)IM_FLAGS * n_pad + i] = flags;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    im[(size_t)(IM_QX + k) * n_pad + i] = x.v[k];
+    im[(size_t)(IM_QY + k) * n_pad + i] = y.v[k];
+    im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    im[(size_t)(IM_K1 + k) * n_pad + i] = k1[k];
+    im[(size_t)(IM_K2 + k) * n_pad + i] = k2[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    im[(size_t)(IM_U1L + k) * n_pad + i] = u1.v[k];
+    im[(size_t)(IM_U1H + k) * n_pad + i] = u1.v[4 + k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 2. ecmult + x compare
+// ---------------------------------------------------------------------------
+HKV_DEV void qtab_store(uint32_t* __restrict__ qs, uint32_t n_lanes, uint32_t lane, int quad, const fe& a) {
+  uint4* p0 = reinterpret_cast<uint4*>(qs) + (size_t)quad * n_lanes + lane;
+  uint4* p1 = reinterpret_cast<uint4*>(qs) + (size_t)(quad + 1) * n_lanes + lane;
+  *p0 = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  *p1 = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32_t lane, int quad, fe& a) {
+  const uint4 v0 = reinterpret_cast<const uint4*>(qs)[(size_t)quad * n_lanes + lane];
+  const uint4 v1 = reinterpret_cast<const uint4*>(qs)[(size_t)(quad + 1) * n_lanes + lane];
+  a.v[0] = v0.x; a.v[1] = v0.y; a.v[2] = v0.z; a.v[3] = v0.w;
+  a.v[4] = v1.x; a.v[5] = v1.y; a.v[6] = v1.z; a.v[7] = v1.w;
+}
+
+// Booth digit from the bits at positions 127..127+W of a left-shifted scalar.
+template <int W>
+HKV_DEV int booth_digit(uint32_t k3, uint32_t k4) {
+  const uint32_t v = (k3 >> 31) | ((k4 & ((1u << W) - 1u)) << 1);
+  return (int)((v + 1u) >> 1) - (int)((v >> W) << W);
+}
+HKV_DEV void shl4(uint32_t K[5]) {
+  K[4] = (K[4] << 4) | (K[3] >> 28);
+  K[3] = (K[3] << 4) | (K[2] >> 28);
+  K[2] = (K[2] << 4) | (K[1] >> 28);
+  K[1] = (K[1] << 4) | (K[0] >> 28);
+  K[0] <<= 4;
+}
+
+__global__ void __launch_bounds__(WG) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
+                                                        uint32_t n_pad, const uint32_t* __restrict__ gtab,
+                                                        uint32_t* __restrict__ qs,
+                                                        uint32_t* __restrict__ bits) {
+  __shared__ __attribute__((aligned(16))) uint32_t gl[GTAB_DWORDS];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(gtab);
+    uint4* dst = reinterpret_cast<uint4*>(gl);
+    for (int k = threadIdx.x; k < GTAB_DWORDS / 4; k += WG) dst[k] = src[k];
+  }
+  __syncthreads();
+
+  const uint32_t n_lanes = gridDim.x * WG;
+  const uint32_t lane = blockIdx.x * WG + threadIdx.x;
+
+  for (uint32_t base = blockIdx.x * WG; base < n_pad; base += gridDim.x * WG) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+    const bool valid = (i < n) && (flags & FLAG_VALID);
+    ge q;
+    uint32_t K1[5], K2[5], KL[5], KH[5];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      q.x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
+      q.y.v[k] = im[(size_t)(IM_QY + k) * n_pad + i];
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      K1[k] = valid ? im[(size_t)(IM_K1 + k) * n_pad + i] : 0u;
+      K2[k] = valid ? im[(size_t)(IM_K2 + k) * n_pad + i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      KL[k] = valid ? im[(size_t)(IM_U1L + k) * n_pad + i] : 0u;
+      KH[k] = valid ? im[(size_t)(IM_U1H + k) * n_pad + i] : 0u;
+    }
+    KL[4] = 0;
+    KH[4] = 0;
+    if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
+    const bool neg1 = (flags & FLAG_NEG1) != 0, neg2 = (flags & FLAG_NEG2) != 0;
+
+    // ---- table: j*Q, j = 1..8, on the isomorphic curve of scale Zg ----
+    // Pass 1 streams raw entries to the lane's scratch (z-ratios H_j parked in
+    // the beta*x slot of entry j-1); pass 2 walks back rescaling every entry
+    // to the common Z (rho_j = prod_{k>j} H_k) and writes beta*x.
+    fe Zg;
+    {
+      gej p2, pj;
+      gej_set_ge(p2, q);
+      gej_double(p2, p2);  // 2Q (Jacobian, scale Z2)
+      fe z2, qx, qy;       // Q' = phi_Z2(Q) = (x Z2^2, y Z2^3)
+      fe_sqr(z2, p2.z);
+      fe_mul(qx, q.x, z2);
+      fe_mul(z2, z2, p2.z);
+      fe_mul(qy, q.y, z2);
+      qtab_store(qs, n_lanes, lane, 0 * QTAB_QUADS_PER_ENTRY + 0, qx);
+      qtab_store(qs, n_lanes, lane, 0 * QTAB_QUADS_PER_ENTRY + 2, qy);
+      qtab_store(qs, n_lanes, lane, 1 * QTAB_QUADS_PER_ENTRY + 0, p2.x);
+      qtab_store(qs, n_lanes, lane, 1 * QTAB_QUADS_PER_ENTRY + 2, p2.y);
+      pj.x = p2.x;
+      pj.y = p2.y;
+      fe_set_u32(pj.z, 1);
+#pragma unroll 1
+      for (int j = 2; j < 8; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
+        bool hz, rz;
+        fe h;
+        gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
+        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 0, pj.x);
+        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 2, pj.y);
+        qtab_store(qs, n_lanes, lane, (j - 1) * QTAB_QUADS_PER_ENTRY + 4, h);
+      }
+      fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
+      fe beta;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) beta.v[k] = FE_BETA[k];
+      {
+        fe bx;
+        fe_mul(bx, pj.x, beta);
+        qtab_store(qs, n_lanes, lane, 7 * QTAB_QUADS_PER_ENTRY + 4, bx);
+      }
+      fe rho;
+      fe_set_u32(rho, 1);
+#pragma unroll 1
+      for (int j = 6; j >= 0; --j) {
+        fe x, y, t;
+        if (j >= 1) {
+          qtab_load(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 4, t);  // H_{j+1}
+          fe_mul(rho, rho, t);
+        }
+        qtab_load(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 0, x);
+        qtab_load(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 2, y);
+        fe_sqr(t, rho);
+        fe_mul(x, x, t);
+        fe_mul(t, t, rho);
+        fe_mul(y, y, t);
+        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 0, x);
+        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 2, y);
+        fe_mul(x, x, beta);
+        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 4, x);
+      }
+    }
+
+    // ---- shared doubling chain, 33 radix-16 windows ----
+    gej acc;
+    bool inf = true;
+    fe_set_zero(acc.x);
+    fe_set_zero(acc.y);
+    fe_set_zero(acc.z);
+    for (int win = 32; win >= 0; --win) {
+      if (win != 32) {
+        for (int d = 0; d < 4; ++d) gej_double(acc, acc);
+      }
+      // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
+#pragma unroll 1
+      for (int slot = 0; slot < 2; ++slot) {
+        const int dg = booth_digit<4>(slot == 0 ? K1[3] : K2[3], slot == 0 ? K1[4] : K2[4]);
+        const bool take = dg != 0;
+        const int mag = dg < 0 ? -dg : dg;
+        const int idx = take ? mag - 1 : 0;
+        const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
+        fe tx, ty;
+        qtab_load(qs, n_lanes, lane, idx * QTAB_QUADS_PER_ENTRY + (slot == 0 ? 0 : 4), tx);
+        qtab_load(qs, n_lanes, lane, idx * QTAB_QUADS_PER_ENTRY + 2, ty);
+        fe nty;
+        fe_neg(nty, ty);
+        fe_cmov(ty, nty, neg);
+        gej_accumulate(acc, inf, acc.z, tx, ty, tx, ty, take);
+      }
+      // G terms every other window: slot 2 = u1_lo * G, slot 3 = u1_hi * 2^128 G
+      if ((win & 1) == 0) {
+#pragma unroll 1
+        for (int slot = 0; slot < 2; ++slot) {
+          const int dg = booth_digit<8>(slot == 0 ? KL[3] : KH[3], slot == 0 ? KL[4] : KH[4]);
+          const bool take = dg != 0;
+          const int mag = dg < 0 ? -dg : dg;
+          const int idx = take ? mag - 1 : 0;
+          const uint32_t* e = gl + (slot * GTAB_ENTRIES + idx) * 16;
+          fe tx, ty;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { tx.v[k] = e[k]; ty.v[k] = e[8 + k]; }
+          fe nty;
+          fe_neg(nty, ty);
+          fe_cmov(ty, nty, dg < 0);
+          fe az;
+          fe_mul(az, acc.z, Zg);
+          fe itx = tx, ity = ty;
+          if (__any(take && inf)) {  // map G-multiple onto the accumulator's curve
+            fe zg2, zg3;
+            fe_sqr(zg2, Zg);
+            fe_mul(zg3, zg2, Zg);
+            fe_mul(itx, tx, zg2);
+            fe_mul(ity, ty, zg3);
+          }
+          gej_accumulate(acc, inf, az, tx, ty, itx, ity, take);
+        }
+      }
+      shl4(K1);
+      shl4(K2);
+      shl4(KL);
+      shl4(KH);
+    }
+
+    // ---- inversion-free x compare ----
+    bool accept = false;
+    {
+      sc r;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r.v[k] = im[(size_t)(IM_R + k) * n_pad + i];
+      fe zt, zz, X, t, rf;
+      fe_mul(zt, acc.z, Zg);
+      fe_sqr(zz, zt);
+      X = acc.x;
+      fe_normalize(X);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rf.v[k] = r.v[k];
+      fe_mul(t, rf, zz);
+      fe_normalize(t);
+      bool eq = fe_eq_norm(t, X);
+      // r + n < p ?
+      const bool small_r = u256_lt(r.v, PMN);
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rf.v[k] = addc(r.v[k], SC_N[k], c);
+      fe_mul(t, rf, zz);
+      fe_normalize(t);
+      eq = eq || (small_r && fe_eq_norm(t, X));
+      accept = valid && !inf && eq;
+    }
+    const uint64_t ball = __ballot(accept);
+    if ((threadIdx.x & 63) == 0) {
+      const uint32_t wbase = base + (threadIdx.x & ~63u);
+      if (wbase < n_pad) {
+        bits[wbase / 32] = (uint32_t)ball;
+        bits[wbase / 32 + 1] = (uint32_t)(ball >> 32);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// shared helpers for table init / generators: simple MSB-first double-and-add
+// with complete additions (slow, used off the timed path only).
+// ---------------------------------------------------------------------------
+HKV_DEV void gej_add_affine_complete(gej& acc, bool& inf, const ge& b, bool take) {
+  gej_accumulate(acc, inf, acc.z, b.x, b.y, b.x, b.y, take);
+}
+// r = a*G + b*P (either scalar may be zero), affine output; returns false if infinity
+HKV_DEV bool ecmult_simple(ge& out, const sc& a, const sc& b, const ge& p) {
+  ge g;
+  ge_set_g(g);
+  gej acc;
+  bool inf = true;
+  fe_set_zero(acc.x);
+  fe_set_zero(acc.y);
+  fe_set_zero(acc.z);
+  for (int bit = 255; bit >= 0; --bit) {
+    if (__any(!inf)) {
+      gej d;
+      gej_double(d, acc);
+      gej_cmov(acc, d, !inf);
+    }
+    const bool ba = (a.v[bit >> 5] >> (bit & 31)) & 1u;
+    const bool bb = (b.v[bit >> 5] >> (bit & 31)) & 1u;
+    gej_add_affine_complete(acc, inf, g, ba);
+    gej_add_affine_complete(acc, inf, p, bb);
+  }
+  if (inf) return false;
+  fe zi, zi2, zi3;
+  fe_inv(zi, acc.z);
+  fe_sqr(zi2, zi);
+  fe_mul(zi3, zi2, zi);
+  fe_mul(out.x, acc.x, zi2);
+  fe_mul(out.y, acc.y, zi3);
+  fe_normalize(out.x);
+  fe_normalize(out.y);
+  return true;
+}
+
+// 3. fixed-base tables: entry j (1..128) of table t = j * (2^(128 t) G)
+__global__ void __launch_bounds__(WG) hkv_gtable_kernel(uint32_t* __restrict__ gtab) {
+  const int tid = blockIdx.x * WG + threadIdx.x;
+  if (tid >= 2 * GTAB_ENTRIES) return;
+  const int t = tid / GTAB_ENTRIES, j = tid % GTAB_ENTRIES + 1;
+  sc a, zero;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { a.v[k] = 0; zero.v[k] = 0; }
+  // scalar j * 2^(128 t)
+  a.v[t * 4] = (uint32_t)j;
+  ge g, out;
+  ge_set_g(g);
+  ecmult_simple(out, a, zero, g);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    gtab[tid * 16 + k] = out.x.v[k];
+    gtab[tid * 16 + 8 + k] = out.y.v[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 4. synthetic batch generator (keyless construction)
+// ---------------------------------------------------------------------------
+HKV_DEV uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+HKV_DEV void rand_scalar(sc& r, uint64_t& st) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t v = splitmix64(st);
+    r.v[2 * k] = (uint32_t)v;
+    r.v[2 * k + 1] = (uint32_t)(v >> 32);
+  }
+  sc_cond_sub_n(r.v);
+  if (u256_is_zero(r.v)) r.v[0] = 1;
+}
+
+__global__ void __launch_bounds__(WG) hkv_gen_pool_kernel(uint64_t seed, uint32_t npool,
+                                                          uint32_t* __restrict__ pool) {
+  const uint32_t j = blockIdx.x * WG + threadIdx.x;
+  if (j >= npool) return;
+  uint64_t st = seed * 0x2545F4914F6CDD1Dull + j * 0x9E3779B97F4A7C15ull + 0x5851F42D4C957F2Dull;
+  sc d, zero;
+  rand_scalar(d, st);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) zero.v[k] = 0;
+  ge g, q;
+  ge_set_g(g);
+  ecmult_simple(q, d, zero, g);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    pool[(size_t)j * 16 + k] = q.x.v[k];
+    pool[(size_t)j * 16 + 8 + k] = q.y.v[k];
+  }
+}
+
+HKV_DEV void put_be256(uint8_t* dst, const uint32_t v[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t x = v[7 - j];
+    dst[4 * j + 0] = (uint8_t)(x >> 24);
+    dst[4 * j + 1] = (uint8_t)(x >> 16);
+    dst[4 * j + 2] = (uint8_t)(x >> 8);
+    dst[4 * j + 3] = (uint8_t)x;
+  }
+}
+
+// Valid (msg32, r, s, Q) without a secret key: R = aG + bQ, r = R.x mod n,
+// s = r/b, msg = a*s; low-S by s -> n-s (verifies with -R, same x).
+__global__ void __launch_bounds__(WG) hkv_gen_records_kernel(uint64_t seed, uint32_t n,
+                                                             const uint32_t* __restrict__ pool,
+                                                             uint32_t npool, uint32_t unc_permille,
+                                                             uint8_t* __restrict__ recs) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st = seed * 0xD1B54A32D192ED03ull + (uint64_t)i * 0x9E3779B97F4A7C15ull + 0x8CB92BA72F3D8DD7ull;
+  sc a, b;
+  rand_scalar(a, st);
+  rand_scalar(b, st);
+  const uint64_t pick = splitmix64(st);
+  const uint32_t j = (uint32_t)(pick % npool);
+  const bool unc = ((pick >> 40) % 1000u) < unc_permille;
+  ge q, R;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    q.x.v[k] = pool[(size_t)j * 16 + k];
+    q.y.v[k] = pool[(size_t)j * 16 + 8 + k];
+  }
+  ecmult_simple(R, a, b, q);
+  sc r, s, bi, m;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = R.x.v[k];
+  sc_cond_sub_n(r.v);
+  sc_inv(bi, b);
+  sc_mul(s, r, bi);
+  sc_mul(m, a, s);                 // msg = a*s BEFORE the low-S flip:
+  if (sc_is_high(s)) sc_neg(s, s);  // (m, r, -s) verifies with -R (same x)
+  uint8_t* o = recs + (size_t)i * REC_SIZE;
+  put_be256(o, m.v);
+  put_be256(o + 32, r.v);
+  put_be256(o + 64, s.v);
+  o[96] = unc ? 65 : 33;
+  if (unc) {
+    o[97] = 4;
+    put_be256(o + 98, q.x.v);
+    put_be256(o + 130, q.y.v);
+  } else {
+    o[97] = (uint8_t)(2u | (q.y.v[0] & 1u));
+    put_be256(o + 98, q.x.v);
+    for (int k = 130; k < 162; ++k) o[k] = 0;
+  }
+  for (int k = 162; k < REC_SIZE; ++k) o[k] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// debug / known-answer kernel for the tests (field, scalar, GLV ops)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(WG) hkv_debug_kernel(uint32_t op, uint32_t n, const uint32_t* __restrict__ a,
+                                                       const uint32_t* __restrict__ b,
+                                                       uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  fe x, y, z;
+  sc u, v, wres;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    x.v[k] = a[i * 8 + k];
+    y.v[k] = b[i * 8 + k];
+    u.v[k] = x.v[k];
+    v.v[k] = y.v[k];
+  }
+  uint32_t res[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) res[k] = 0;
+  switch (op) {
+    case HKV_DBG_FE_MUL: fe_mul(z, x, y); fe_normalize(z); for (int k = 0; k < 8; ++k) res[k] = z.v[k]; break;
+    case HKV_DBG_FE_SQR: fe_sqr(z, x); fe_normalize(z); for (int k = 0; k < 8; ++k) res[k] = z.v[k]; break;
+    case HKV_DBG_FE_ADD: fe_add(z, x, y); fe_normalize(z); for (int k = 0; k < 8; ++k) res[k] = z.v[k]; break;
+    case HKV_DBG_FE_SUB: fe_sub(z, x, y); fe_normalize(z); for (int k = 0; k < 8; ++k) res[k] = z.v[k]; break;
+    case HKV_DBG_FE_INV: fe_inv(z, x); fe_normalize(z); for (int k = 0; k < 8; ++k) res[k] = z.v[k]; break;
+    case HKV_DBG_FE_SQRT: fe_sqrt_cand(z, x); fe_normalize(z); for (int k = 0; k < 8; ++k) res[k] = z.v[k]; break;
+    case HKV_DBG_SC_MUL: sc_mul(wres, u, v); for (int k = 0; k < 8; ++k) res[k] = wres.v[k]; break;
+    case HKV_DBG_SC_INV: sc_inv(wres, u); for (int k = 0; k < 8; ++k) res[k] = wres.v[k]; break;
+    case HKV_DBG_GLV: {
+      uint32_t k1[5], k2[5];
+      bool n1, n2;
+      const bool okk = glv_split(u, k1, n1, k2, n2);
+      for (int k = 0; k < 5; ++k) { res[k] = k1[k]; res[5 + k] = k2[k]; }
+      res[10] = (n1 ? 1u : 0u) | (n2 ? 2u : 0u) | (okk ? 0u : 4u);
+      break;
+    }
+    case HKV_DBG_ECMULT_G: {  // x-only affine of u*G (+ y)
+      ge g, o;
+      sc zero;
+      for (int k = 0; k < 8; ++k) zero.v[k] = 0;
+      ge_set_g(g);
+      const bool okk = ecmult_simple(o, u, zero, g);
+      for (int k = 0; k < 8; ++k) { res[k] = o.x.v[k]; res[8 + k] = o.y.v[k]; }
+      if (!okk) res[15] ^= 0xFFFFFFFFu;
+      break;
+    }
+    default: break;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[i * 16 + k] = res[k];
+}
+
+}  // namespace hkv
+
+// ---------------------------------------------------------------------------
+// launch wrappers (called by hkv_api.cpp)
+// ---------------------------------------------------------------------------
+namespace hkv {
+
+static inline uint32_t ceil_div(size_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(hkv_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st,
+                     (const uint32_t*)recs, n, n_pad, mode, im);
+  return hipGetLastError();
+}
+hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
+                         uint32_t grid, uint32_t* bits, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_ecmult_kernel, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits);
+  return hipGetLastError();
+}
+hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div(2 * GTAB_ENTRIES, WG)), dim3(WG), 0, st, gtab);
+  return hipGetLastError();
+}
+hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_gen_pool_kernel, dim3(ceil_div(npool, WG)), dim3(WG), 0, st, seed, npool, pool);
+  return hipGetLastError();
+}
+hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,
+                              uint32_t unc_permille, void* recs, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_gen_records_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, seed, n, pool, npool,
+                     unc_permille, (uint8_t*)recs);
+  return hipGetLastError();
+}
+hipError_t launch_debug(uint32_t op, uint32_t n, const uint32_t* a, const uint32_t* b, uint32_t* out,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(hkv_debug_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, op, n, a, b, out);
+  return hipGetLastError();
+}
+hipError_t ecmult_max_blocks_per_cu(int* out) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel, WG, 0);
+}
+
+}  // namespace hkv

@@ -1,0 +1,85 @@
+"""ctypes binding of libhkv.so (include/hkv.h). One definition per exported
+symbol, mirroring the header; ``EXPORTS`` is checked against the header by
+``tests/test_abi.py``."""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+HKV_RECORD_SIZE = 168
+HKV_LIBSECP = 0
+HKV_HASKOIN = 1
+
+HKV_OK = 0
+_ERRS = {-1: "HKV_E_ARG", -2: "HKV_E_NODEV", -3: "HKV_E_OOM", -4: "HKV_E_HIP", -5: "HKV_E_INTERNAL"}
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lib_path() -> str:
+    return os.environ.get("HKV_LIB", os.path.join(_PKG_DIR, "lib", "libhkv.so"))
+
+
+class HkvError(RuntimeError):
+    def __init__(self, rc: int, what: str, lib=None):
+        detail = ""
+        if lib is not None:
+            try:
+                detail = lib.hkv_last_hip_error().decode()
+            except Exception:  # pragma: no cover - best effort
+                detail = ""
+        super().__init__(f"{what}: {_ERRS.get(rc, rc)} {detail}".strip())
+        self.rc = rc
+
+
+# name -> (restype, argtypes)
+EXPORTS = {
+    "hkv_open": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
+    "hkv_open_devices": (c_int, [POINTER(c_int), c_int, c_uint32, POINTER(c_void_p)]),
+    "hkv_close": (None, [c_void_p]),
+    "hkv_ctx_num_devices": (c_int, [c_void_p]),
+    "hkv_batch_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "hkv_batch_free": (None, [c_void_p]),
+    "hkv_batch_records": (POINTER(c_uint8), [c_void_p]),
+    "hkv_batch_capacity": (c_size_t, [c_void_p]),
+    "hkv_verify": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, POINTER(c_uint32)]),
+    "hkv_verify_host": (c_int, [c_void_p, c_void_p, c_size_t, c_uint32, POINTER(c_uint32)]),
+    "hkv_verify_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint32, c_void_p, c_void_p]),
+    "hkv_gen_records_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_uint32, c_uint32, c_void_p,
+                                       c_void_p]),
+    "hkv_debug_op": (c_int, [c_void_p, c_int, c_uint32, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hkv_profile_enable": (c_int, [c_void_p, c_int]),
+    "hkv_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
+                                 POINTER(c_uint64)]),
+    "hkv_strerror": (c_char_p, [c_int]),
+    "hkv_last_hip_error": (c_char_p, []),
+    "hkv_device_count": (c_int, []),
+    "hkv_version": (c_uint32, []),
+}
+
+_LIB = None
+
+
+def load_library(path: str | None = None):
+    """Load libhkv.so and bind every export. Raises if the library is absent:
+    the product path has no fallback."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or lib_path()
+    if not os.path.exists(p):
+        raise ImportError(f"libhkv.so not built at {p}; run __graft_entry__.build()")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str, lib=None) -> None:
+    if rc != HKV_OK:
+        raise HkvError(rc, what, lib)

@@ -1,0 +1,126 @@
+/*
+ * hkv.h — C ABI of libhkv: MI355X batch secp256k1 ECDSA verification.
+ *
+ * Drop-in boundary for the signature-check hot path of a haskoin-node based
+ * validator. What each entry point replaces:
+ *
+ *   hkv_verify / hkv_verify_device
+ *       replaces N per-input calls of haskoin-core
+ *       `verifyHashSig :: Ctx -> Hash256 -> Sig -> PubKey -> Bool`
+ *       (Haskoin.Crypto.Signature, haskoin-core-1.1.0 pinned at
+ *       /root/reference/stack.yaml:10) in mode HKV_HASKOIN, and of
+ *       secp256k1-haskell `verifySig` -> FFI `secp256k1_ecdsa_verify`
+ *       (secp256k1-haskell-1.2.0, /root/reference/stack.yaml:9) in mode
+ *       HKV_LIBSECP. Per-record parsing replaces `importPubKey`
+ *       (secp256k1_ec_pubkey_parse) and `importCompactSig`
+ *       (secp256k1_ecdsa_signature_parse_compact) so raw/adversarial bytes
+ *       get exact reject parity. The reference itself never verifies; the
+ *       batch is fed from the node's block/tx events
+ *       (/root/reference/src/Haskoin/Node.hs:151-174, Peer.hs:309-344).
+ *   hkv_open / hkv_close
+ *       replaces secp256k1-haskell `createContext`/`withContext` (one
+ *       shared read-only context per process).
+ *
+ * Conventions: no C++ exceptions cross this boundary; every function that
+ * can fail returns 0 (HKV_OK) or a negative hkv_err. A verdict is never an
+ * error: malformed records simply get bit 0. Verdict bit i of the output is
+ * bit (i % 32) of word (i / 32); 1 = accept.
+ *
+ * Record layout (HKV_RECORD_SIZE = 168 bytes, 8-byte aligned array):
+ *   [0,32)    msg32   (the Hash256 bytes as secp256k1 `msg32`, no reversal)
+ *   [32,64)   r       big-endian (compact signature first half)
+ *   [64,96)   s       big-endian
+ *   [96]      pubkey length in bytes (33 or 65 are the only valid ones)
+ *   [97,162)  pubkey  SEC1 bytes (02/03 compressed, 04 uncompressed,
+ *                     06/07 hybrid), zero padded
+ *   [162,168) zero padding
+ */
+#ifndef HKV_H
+#define HKV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HKV_RECORD_SIZE 168
+
+/* verify modes */
+#define HKV_LIBSECP 0u /* secp256k1_ecdsa_verify: high-S rejected        */
+#define HKV_HASKOIN 1u /* verifyHashSig: normalize to low-S, then verify */
+
+enum hkv_err {
+  HKV_OK = 0,
+  HKV_E_ARG = -1,      /* bad argument (NULL, n > capacity, bad mode)   */
+  HKV_E_NODEV = -2,    /* no usable gfx950 device                       */
+  HKV_E_OOM = -3,      /* device or pinned host allocation failed       */
+  HKV_E_HIP = -4,      /* HIP runtime error (see hkv_last_hip_error)     */
+  HKV_E_INTERNAL = -5, /* self-check failed at open                      */
+};
+
+typedef struct hkv_ctx hkv_ctx;
+typedef struct hkv_batch hkv_batch;
+
+/* open flags */
+#define HKV_OPEN_NO_SELFCHECK 1u /* skip the known-answer self-check at open */
+
+/* Open a context on the first n_gpus visible devices (n_gpus <= 0: all).
+ * Builds the fixed-base tables on every device and, unless flags has
+ * HKV_OPEN_NO_SELFCHECK, verifies 256 generated signatures per device
+ * (HKV_E_INTERNAL if any is rejected). */
+int hkv_open(int n_gpus, uint32_t flags, hkv_ctx** out);
+/* Open on an explicit list of HIP device ordinals (one process per GPU:
+ * pass {LOCAL_RANK}). Context device index k refers to device_ids[k]. */
+int hkv_open_devices(const int* device_ids, int n_ids, uint32_t flags, hkv_ctx** out);
+void hkv_close(hkv_ctx* ctx);
+int hkv_ctx_num_devices(const hkv_ctx* ctx);
+
+/* Pinned host record buffer with room for max_n records. */
+int hkv_batch_alloc(hkv_ctx* ctx, size_t max_n, hkv_batch** out);
+void hkv_batch_free(hkv_batch* b);
+uint8_t* hkv_batch_records(hkv_batch* b);
+size_t hkv_batch_capacity(const hkv_batch* b);
+
+/* Verify records [0, n) of the batch. Shards contiguous 64-aligned index
+ * ranges across the context's devices; writes ceil(n/32) words. Blocking. */
+int hkv_verify(hkv_ctx* ctx, hkv_batch* b, size_t n, uint32_t mode, uint32_t* verdict_bits);
+
+/* Same, from any host memory (copied through the context's staging). */
+int hkv_verify_host(hkv_ctx* ctx, const uint8_t* records, size_t n, uint32_t mode, uint32_t* verdict_bits);
+
+/* Device-resident form: d_records (n * 168 bytes) and d_bits
+ * (>= ceil(n/64)*2 words) live in HBM of the context's device `dev`; work is
+ * enqueued on `hip_stream` (NULL = default stream) and NOT synchronised.
+ * Used by one-process-per-GPU sharding (bench.py) and by zero-copy callers. */
+int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, uint32_t mode,
+                      uint32_t* d_bits, void* hip_stream);
+
+/* Synthetic valid records (keyless construction) written
+ * to device memory: pubkeys from a pool of `pool_size` keys, a per-mille
+ * share of uncompressed keys, all signatures low-S. Enqueued on hip_stream. */
+int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
+                           uint32_t uncompressed_permille, void* d_records, void* hip_stream);
+
+/* Known-answer hook for the tests: applies op (see hkv_internal.h) to n
+ * pairs of 8-limb little-endian operands in device memory; 16 words out. */
+int hkv_debug_op(hkv_ctx* ctx, int dev, uint32_t op, size_t n, const uint32_t* d_a, const uint32_t* d_b,
+                 uint32_t* d_out, void* hip_stream);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around the
+ * prologue and ecmult kernels of every subsequent verify (bench.py's roofline).
+ * read: synchronises, returns summed milliseconds and the launch count, resets. */
+int hkv_profile_enable(hkv_ctx* ctx, int on);
+int hkv_profile_read(hkv_ctx* ctx, int dev, double* prologue_ms, double* ecmult_ms, uint64_t* launches);
+
+const char* hkv_strerror(int err);
+const char* hkv_last_hip_error(void);
+int hkv_device_count(void);
+/* ABI version: (major << 16) | minor */
+uint32_t hkv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HKV_H */

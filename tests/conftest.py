@@ -1,0 +1,57 @@
+"""Shared test setup. GPU tests are marked ``@pytest.mark.gpu`` and run only
+on the MI355X box (``pytest -m gpu``); everything else runs on CPU."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "haskoin-node_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libhkv_oracle.so")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def kat():
+    """Golden KAT records + manifest (tests/golden/make_golden.py)."""
+    with open(os.path.join(GOLDEN, "kat_manifest.json")) as f:
+        man = json.load(f)
+    data = open(os.path.join(GOLDEN, "kat_records.bin"), "rb").read()
+    assert len(data) == man["count"] * man["record_size"]
+    recs = [data[i * 168:(i + 1) * 168] for i in range(man["count"])]
+    return recs, man["records"]
+
+
+@pytest.fixture(scope="session")
+def coracle():
+    """The C restatement (oracle/hkv_oracle.c), built by __graft_entry__.build()."""
+    import ctypes
+    if not os.path.exists(ORACLE_SO):
+        import subprocess
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                       stdout=subprocess.DEVNULL)
+    lib = ctypes.CDLL(ORACLE_SO)
+    lib.hkvo_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_int]
+    lib.hkvo_verify_record.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.hkvo_pubkey_parse.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+    return lib
+
+
+def oracle_batch(lib, recs_bytes: bytes, mode: int, threads: int = 8):
+    import ctypes
+    import numpy as np
+    n = len(recs_bytes) // 168
+    out = np.zeros(n, dtype=np.uint8)
+    buf = np.frombuffer(recs_bytes, dtype=np.uint8)
+    lib.hkvo_verify_batch(buf.ctypes.data_as(ctypes.c_void_p), n, mode,
+                          out.ctypes.data_as(ctypes.c_void_p), threads)
+    return out.astype(bool)
