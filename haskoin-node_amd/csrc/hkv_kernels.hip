@@ -120,34 +120,122 @@ __global__ void __launch_bounds__(WG) hkv_prologue_kernel(const uint32_t* __rest
   }
   ok = ok && pk_ok;
 
-  // --- scalars: s^-1, u1, u2, GLV split of u2
-  sc sinv, u1, u2;
-  sc_inv(sinv, s);
-  sc_mul(u1, m, sinv);
-  sc_mul(u2, r, sinv);
-  uint32_t k1[5], k2[5];
-  bool n1, n2;
-  const bool glv_ok = glv_split(u2, k1, n1, k2, n2);
-
-  uint32_t flags = (ok ? FLAG_VALID : 0u) | (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) |
-                   (glv_ok ? 0u : FLAG_GLV_OVF);
-  if (!glv_ok) flags &= ~FLAG_VALID;  // unreachable for a correct basis; fail closed
+  const uint32_t flags = ok ? FLAG_VALID : 0u;
   im[(size_t)IM_FLAGS * n_pad + i] = flags;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     im[(size_t)(IM_QX + k) * n_pad + i] = x.v[k];
     im[(size_t)(IM_QY + k) * n_pad + i] = y.v[k];
     im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
+    im[(size_t)(IM_S + k) * n_pad + i] = s.v[k];
+    im[(size_t)(IM_M + k) * n_pad + i] = m.v[k];
   }
+}
+
+// ---------------------------------------------------------------------------
+// 1b. scalar kernel: s^-1 by Montgomery's batch trick over BATCH_INV
+//     signatures per thread (strided for coalescing), then u1 = m/s,
+//     u2 = r/s and the GLV split of u2.
+// ---------------------------------------------------------------------------
+HKV_DEV void im_load8(const uint32_t* __restrict__ im, uint32_t n_pad, int w, uint32_t i, uint32_t* v) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    im[(size_t)(IM_K1 + k) * n_pad + i] = k1[k];
-    im[(size_t)(IM_K2 + k) * n_pad + i] = k2[k];
+  for (int k = 0; k < 8; ++k) v[k] = im[(size_t)(w + k) * n_pad + i];
+}
+HKV_DEV void im_store8(uint32_t* __restrict__ im, uint32_t n_pad, int w, uint32_t i, const uint32_t* v) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) im[(size_t)(w + k) * n_pad + i] = v[k];
+}
+
+template <int L>
+HKV_DEV void shr_bits(uint32_t* a, int b) {
+#pragma unroll
+  for (int q = 0; q < L - 1; ++q) a[q] = (a[q] >> b) | (a[q + 1] << (32 - b));
+  a[L - 1] >>= b;
+}
+// Radix-16 / radix-256 Booth recoding (LSB first, MSB-first consumption in
+// the ecmult kernel): d = ((v + 1) >> 1) - ((v >> W) << W), v = bits
+// [pos-1, pos+W-1]; sum_w d_w 16^w reproduces the scalar (< 2^131).
+HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2,
+                          uint32_t* SL, uint32_t* SH) {
+  uint32_t p1 = 0, p2 = 0, pl = 0, ph = 0;
+#pragma unroll 1
+  for (int w = 0; w < NWIN; ++w) {
+    const uint32_t v1 = p1 | ((S1[0] & 15u) << 1), v2 = p2 | ((S2[0] & 15u) << 1);
+    p1 = (S1[0] >> 3) & 1u;
+    p2 = (S2[0] >> 3) & 1u;
+    shr_bits<5>(S1, 4);
+    shr_bits<5>(S2, 4);
+    const int d1 = (int)((v1 + 1u) >> 1) - (int)((v1 >> 4) << 4);
+    const int d2 = (int)((v2 + 1u) >> 1) - (int)((v2 >> 4) << 4);
+    int dl = 0, dh = 0;
+    if ((w & 1) == 0) {
+      const uint32_t vl = pl | ((SL[0] & 255u) << 1), vh = ph | ((SH[0] & 255u) << 1);
+      pl = (SL[0] >> 7) & 1u;
+      ph = (SH[0] >> 7) & 1u;
+      shr_bits<4>(SL, 8);
+      shr_bits<4>(SH, 8);
+      dl = (int)((vl + 1u) >> 1) - (int)((vl >> 8) << 8);
+      dh = (int)((vh + 1u) >> 1) - (int)((vh >> 8) << 8);
+    }
+    im[(size_t)(IM_DIG + w) * n_pad + i] = (uint32_t)(d1 + 8) | ((uint32_t)(d2 + 8) << 5) |
+                                           ((uint32_t)(dl + 128) << 10) | ((uint32_t)(dh + 128) << 19);
   }
+}
+
+__global__ void __launch_bounds__(WG) hkv_scalar_kernel(uint32_t n_pad, uint32_t stride, uint32_t* __restrict__ im) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= stride) return;
+  // forward: prefix products c_k = s_0 * ... * s_k (invalid lanes use s = 1)
+  sc c;
+  sc_set_u32(c, 1);
+#pragma unroll 1
+  for (int k = 0; k < BATCH_INV; ++k) {
+    const uint32_t i = t + (uint32_t)k * stride;
+    if (i >= n_pad) break;
+    sc sv;
+    im_load8(im, n_pad, IM_S, i, sv.v);
+    const bool valid = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_VALID) != 0;
+    if (!valid) sc_set_u32(sv, 1);
+    sc_mul(c, c, sv);
+    im_store8(im, n_pad, IM_C, i, c.v);
+  }
+  sc inv;
+  sc_inv(inv, c);
+  // backward: s_k^-1 = inv * c_{k-1}; inv *= s_k
+#pragma unroll 1
+  for (int k = BATCH_INV - 1; k >= 0; --k) {
+    const uint32_t i = t + (uint32_t)k * stride;
+    if (i >= n_pad) continue;
+    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+    const bool valid = (flags & FLAG_VALID) != 0;
+    sc prev, sv, sinv;
+    if (k > 0) {
+      im_load8(im, n_pad, IM_C, i - stride, prev.v);
+    } else {
+      sc_set_u32(prev, 1);
+    }
+    sc_mul(sinv, inv, prev);
+    im_load8(im, n_pad, IM_S, i, sv.v);
+    if (!valid) sc_set_u32(sv, 1);
+    sc_mul(inv, inv, sv);
+    sc m, r, u1, u2;
+    im_load8(im, n_pad, IM_M, i, m.v);
+    im_load8(im, n_pad, IM_R, i, r.v);
+    sc_mul(u1, m, sinv);
+    sc_mul(u2, r, sinv);
+    uint32_t k1[5], k2[5];
+    bool n1, n2;
+    const bool glv_ok = glv_split(u2, k1, n1, k2, n2);
+    uint32_t f = flags | (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
+    if (!glv_ok) f &= ~FLAG_VALID;  // unreachable for a correct basis; fail closed
+    im[(size_t)IM_FLAGS * n_pad + i] = f;
+    const bool use = (f & FLAG_VALID) != 0;
+    uint32_t S1[5], S2[5], SL[4], SH[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    im[(size_t)(IM_U1L + k) * n_pad + i] = u1.v[k];
-    im[(size_t)(IM_U1H + k) * n_pad + i] = u1.v[4 + k];
+    for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
+    write_digits(im, n_pad, i, S1, S2, SL, SH);
   }
 }
 
@@ -167,21 +255,7 @@ HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32
   a.v[4] = v1.x; a.v[5] = v1.y; a.v[6] = v1.z; a.v[7] = v1.w;
 }
 
-// Booth digit from the bits at positions 127..127+W of a left-shifted scalar.
-template <int W>
-HKV_DEV int booth_digit(uint32_t k3, uint32_t k4) {
-  const uint32_t v = (k3 >> 31) | ((k4 & ((1u << W) - 1u)) << 1);
-  return (int)((v + 1u) >> 1) - (int)((v >> W) << W);
-}
-HKV_DEV void shl4(uint32_t K[5]) {
-  K[4] = (K[4] << 4) | (K[3] >> 28);
-  K[3] = (K[3] << 4) | (K[2] >> 28);
-  K[2] = (K[2] << 4) | (K[1] >> 28);
-  K[1] = (K[1] << 4) | (K[0] >> 28);
-  K[0] <<= 4;
-}
-
-__global__ void __launch_bounds__(WG) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
+__global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits) {
@@ -201,24 +275,11 @@ __global__ void __launch_bounds__(WG) hkv_ecmult_kernel(const uint32_t* __restri
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
     ge q;
-    uint32_t K1[5], K2[5], KL[5], KH[5];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       q.x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
       q.y.v[k] = im[(size_t)(IM_QY + k) * n_pad + i];
     }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      K1[k] = valid ? im[(size_t)(IM_K1 + k) * n_pad + i] : 0u;
-      K2[k] = valid ? im[(size_t)(IM_K2 + k) * n_pad + i] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      KL[k] = valid ? im[(size_t)(IM_U1L + k) * n_pad + i] : 0u;
-      KH[k] = valid ? im[(size_t)(IM_U1H + k) * n_pad + i] : 0u;
-    }
-    KL[4] = 0;
-    KH[4] = 0;
     if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
     const bool neg1 = (flags & FLAG_NEG1) != 0, neg2 = (flags & FLAG_NEG2) != 0;
 
@@ -284,43 +345,65 @@ __global__ void __launch_bounds__(WG) hkv_ecmult_kernel(const uint32_t* __restri
     }
 
     // ---- shared doubling chain, 33 radix-16 windows ----
+    // Window w's digit word and the two Q-table entries it selects are
+    // loaded before the window's four doublings, hiding their latency.
     gej acc;
     bool inf = true;
     fe_set_zero(acc.x);
     fe_set_zero(acc.y);
     fe_set_zero(acc.z);
-    for (int win = 32; win >= 0; --win) {
-      if (win != 32) {
+    uint32_t dw = valid ? im[(size_t)(IM_DIG + NWIN - 1) * n_pad + i] : DIG_ZERO;
+#pragma unroll 1
+    for (int win = NWIN - 1; win >= 0; --win) {
+      const int d1 = (int)(dw & 31u) - 8, d2 = (int)((dw >> 5) & 31u) - 8;
+      fe t1x, t1y, t2x, t2y;
+      {
+        const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
+        const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
+        qtab_load(qs, n_lanes, lane, i1 * QTAB_QUADS_PER_ENTRY + 0, t1x);
+        qtab_load(qs, n_lanes, lane, i1 * QTAB_QUADS_PER_ENTRY + 2, t1y);
+        qtab_load(qs, n_lanes, lane, i2 * QTAB_QUADS_PER_ENTRY + 4, t2x);
+        qtab_load(qs, n_lanes, lane, i2 * QTAB_QUADS_PER_ENTRY + 2, t2y);
+      }
+      const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
+      if (win != NWIN - 1) {
+#pragma unroll 1
         for (int d = 0; d < 4; ++d) gej_double(acc, acc);
       }
       // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
 #pragma unroll 1
       for (int slot = 0; slot < 2; ++slot) {
-        const int dg = booth_digit<4>(slot == 0 ? K1[3] : K2[3], slot == 0 ? K1[4] : K2[4]);
+        const int dg = slot == 0 ? d1 : d2;
         const bool take = dg != 0;
-        const int mag = dg < 0 ? -dg : dg;
-        const int idx = take ? mag - 1 : 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
         fe tx, ty;
-        qtab_load(qs, n_lanes, lane, idx * QTAB_QUADS_PER_ENTRY + (slot == 0 ? 0 : 4), tx);
-        qtab_load(qs, n_lanes, lane, idx * QTAB_QUADS_PER_ENTRY + 2, ty);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          tx.v[k] = slot == 0 ? t1x.v[k] : t2x.v[k];
+          ty.v[k] = slot == 0 ? t1y.v[k] : t2y.v[k];
+        }
         fe nty;
         fe_neg(nty, ty);
         fe_cmov(ty, nty, neg);
         gej_accumulate(acc, inf, acc.z, tx, ty, tx, ty, take);
       }
-      // G terms every other window: slot 2 = u1_lo * G, slot 3 = u1_hi * 2^128 G
+      // G terms every other window: slot 0 = u1_lo * G, slot 1 = u1_hi * 2^128 G
       if ((win & 1) == 0) {
 #pragma unroll 1
         for (int slot = 0; slot < 2; ++slot) {
-          const int dg = booth_digit<8>(slot == 0 ? KL[3] : KH[3], slot == 0 ? KL[4] : KH[4]);
+          const int dg = (int)((dw >> (slot == 0 ? 10 : 19)) & 511u) - 128;
           const bool take = dg != 0;
           const int mag = dg < 0 ? -dg : dg;
           const int idx = take ? mag - 1 : 0;
-          const uint32_t* e = gl + (slot * GTAB_ENTRIES + idx) * 16;
+          const uint4* e = reinterpret_cast<const uint4*>(gl + (slot * GTAB_ENTRIES + idx) * 16);
           fe tx, ty;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { tx.v[k] = e[k]; ty.v[k] = e[8 + k]; }
+          {
+            const uint4 a0 = e[0], a1 = e[1], a2 = e[2], a3 = e[3];
+            tx.v[0] = a0.x; tx.v[1] = a0.y; tx.v[2] = a0.z; tx.v[3] = a0.w;
+            tx.v[4] = a1.x; tx.v[5] = a1.y; tx.v[6] = a1.z; tx.v[7] = a1.w;
+            ty.v[0] = a2.x; ty.v[1] = a2.y; ty.v[2] = a2.z; ty.v[3] = a2.w;
+            ty.v[4] = a3.x; ty.v[5] = a3.y; ty.v[6] = a3.z; ty.v[7] = a3.w;
+          }
           fe nty;
           fe_neg(nty, ty);
           fe_cmov(ty, nty, dg < 0);
@@ -337,10 +420,7 @@ __global__ void __launch_bounds__(WG) hkv_ecmult_kernel(const uint32_t* __restri
           gej_accumulate(acc, inf, az, tx, ty, itx, ity, take);
         }
       }
-      shl4(K1);
-      shl4(K2);
-      shl4(KL);
-      shl4(KH);
+      dw = dw_next;
     }
 
     // ---- inversion-free x compare ----
@@ -602,6 +682,10 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
                            hipStream_t st) {
   hipLaunchKernelGGL(hkv_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st,
                      (const uint32_t*)recs, n, n_pad, mode, im);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t stride = ceil_div(n_pad, BATCH_INV);
+  hipLaunchKernelGGL(hkv_scalar_kernel, dim3(ceil_div(stride, WG)), dim3(WG), 0, st, n_pad, stride, im);
   return hipGetLastError();
 }
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,

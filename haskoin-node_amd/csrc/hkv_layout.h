@@ -18,8 +18,24 @@ enum : int {
   IM_U1L = 27,    // 4 limbs, u1 bits 0..127
   IM_U1H = 31,    // 4 limbs, u1 bits 128..255
   IM_R = 35,      // 8 limbs, r (< n)
-  IM_WORDS = 43,
+  IM_C = 43,      // 8 limbs, batch-inversion prefix product (scalar kernel scratch)
+  IM_DIG = 51,    // 33 words: window w's Booth digits (see DIG_* below)
+  IM_WORDS = 84,
+  // between the parse and scalar kernels: s (normalised) and m = msg mod n
+  IM_S = IM_K1,   // 8 limbs over K1|K2 (10 words)
+  IM_M = IM_U1L,  // 8 limbs over U1L|U1H
 };
+// Digit word of window w (w = 0..32, bit position 4w): biased Booth digits
+//   bits 0-4   d1 + 8    (k1, radix 16, -8..8)
+//   bits 5-9   d2 + 8    (k2, radix 16)
+//   bits 10-18 dl + 128  (u1 bits 0..127, radix 256, even w only, else 0)
+//   bits 19-27 dh + 128  (u1 bits 128..255, radix 256, even w only)
+constexpr int NWIN = 33;
+constexpr uint32_t DIG_ZERO = 8u | (8u << 5) | (128u << 10) | (128u << 19);
+
+// signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
+// Montgomery's trick: 3(B-1) multiplications + 1 inversion)
+constexpr int BATCH_INV = 8;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
 // Fixed-base tables: odd/even multiples j*B for j = 1..128, B in {G, 2^128 G},
@@ -36,5 +52,10 @@ constexpr int QTAB_QUADS_PER_ENTRY = 6;
 constexpr int QTAB_QUADS = QTAB_ENTRIES * QTAB_QUADS_PER_ENTRY;
 
 constexpr int WG = 256;                // threads per workgroup (4 waves)
+
+// minimum waves per SIMD the ecmult kernel's register allocation targets
+#ifndef HKV_ECMULT_WAVES
+#define HKV_ECMULT_WAVES 2
+#endif
 
 }  // namespace hkv

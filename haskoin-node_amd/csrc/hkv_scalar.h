@@ -19,6 +19,11 @@ __constant__ static const uint32_t SC_HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x5
 // NC = 2^256 - n, low 4 limbs (the fifth limb is 1)
 constexpr uint32_t NC0 = 0x2FC9BEBFu, NC1 = 0x402DA173u, NC2 = 0x50B75FC4u, NC3 = 0x45512319u;
 
+HKV_DEV void sc_set_u32(sc& r, uint32_t x) {
+  r.v[0] = x;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) r.v[i] = 0;
+}
 HKV_DEV bool u256_lt(const uint32_t* a, const uint32_t* b) {
   uint32_t bw = 0;
 #pragma unroll
