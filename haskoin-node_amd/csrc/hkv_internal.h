@@ -18,6 +18,7 @@ enum {
   HKV_DBG_SC_INV = 8,
   HKV_DBG_GLV = 9,
   HKV_DBG_ECMULT_G = 10,
+  HKV_DBG_MUL512 = 11,
 };
 
 namespace hkv {

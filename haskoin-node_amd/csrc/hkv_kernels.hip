@@ -663,6 +663,7 @@ __global__ void __launch_bounds__(WG) hkv_debug_kernel(uint32_t op, uint32_t n, 
       if (!okk) res[15] ^= 0xFFFFFFFFu;
       break;
     }
+    case HKV_DBG_MUL512: mul512(res, x.v, y.v); break;
     default: break;
   }
 #pragma unroll

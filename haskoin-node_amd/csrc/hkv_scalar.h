@@ -125,7 +125,7 @@ HKV_DEV void sc_reduce512(sc& r, const uint32_t t[16]) {
 
 HKV_DEV void sc_mul(sc& r, const sc& a, const sc& b) {
   uint32_t t[16];
-  mul256(t, a.v, b.v);
+  mul512(t, a.v, b.v);
   sc_reduce512(r, t);
 }
 HKV_DEV void sc_sqr(sc& r, const sc& a) {

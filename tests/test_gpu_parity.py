@@ -13,7 +13,7 @@ from conftest import oracle_batch
 pytestmark = pytest.mark.gpu
 
 HKV_DBG = dict(FE_MUL=1, FE_SQR=2, FE_ADD=3, FE_SUB=4, FE_INV=5, FE_SQRT=6, SC_MUL=7, SC_INV=8, GLV=9,
-               ECMULT_G=10)
+               ECMULT_G=10, MUL512=11)
 
 
 @pytest.fixture(scope="module")
@@ -69,6 +69,17 @@ def test_field_ops_known_answers(torch, ver):
         out = run_debug(torch, ver, op, xs, ys)
         for i in range(len(xs)):
             assert from_limbs(out[i, :8]) == f(xs[i], ys[i]), (op, hex(xs[i]), hex(ys[i]))
+
+
+def test_mul512_product(torch, ver):
+    """Raw 256x256 -> 512-bit limb product (the inline-asm product scanner)."""
+    rng = random.Random(7)
+    xs, ys = rand_vals(rng, 4096), rand_vals(rng, 4096)[::-1]
+    xs += [2**256 - 1] * 4
+    ys += [2**256 - 1, 1, 0, 2**255]
+    out = run_debug(torch, ver, "MUL512", xs, ys)
+    for i in range(len(xs)):
+        assert from_limbs(list(out[i, :8])) + (from_limbs(list(out[i, 8:16])) << 256) == xs[i] * ys[i]
 
 
 def test_field_inv_sqrt(torch, ver):
