@@ -38,27 +38,27 @@ HKV_DEV void gej_cmov(gej& r, const gej& a, bool f) {
   fe_cmov(r.z, a.z, f);
 }
 
-// r = 2a (dbl-2009-l, 2M + 5S). a must not be the point at infinity; y != 0
-// always holds on secp256k1 (no 2-torsion). r may alias a.
+// r = 2a for a = 0 (3M + 4S): A = X^2, B = Y^2, C = B^2, M = X*B (so the
+// usual D = 2((X+B)^2 - A - C) = 4M), E = 3A, F = E^2, X3 = F - 8M,
+// Y3 = E(4M - X3) - 8C, Z3 = 2YZ. On this ISA a product costs about a square,
+// so X*B beats the square-and-subtract form; the power-of-two scalings are
+// funnel shifts. a must not be infinity; y != 0 on secp256k1. r may alias a.
 HKV_DEV void gej_double(gej& r, const gej& a) {
-  fe A, B, C, D, E, t;
+  fe A, B, C, M, E, t;
   fe_sqr(A, a.x);
   fe_sqr(B, a.y);
+  fe_mul(M, a.x, B);
   fe_sqr(C, B);
-  fe_add(t, a.x, B);
-  fe_sqr(t, t);
-  fe_sub(t, t, A);
-  fe_sub(t, t, C);
-  fe_add(D, t, t);          // D = 2((X+B)^2 - A - C)
   fe_mul_small(E, A, 3);    // E = 3A
   fe_mul(r.z, a.y, a.z);
-  fe_add(r.z, r.z, r.z);    // Z3 = 2YZ
+  fe_shl(r.z, r.z, 1);      // Z3 = 2YZ
   fe_sqr(t, E);             // F = E^2
-  fe_sub(t, t, D);
-  fe_sub(r.x, t, D);        // X3 = F - 2D
-  fe_sub(t, D, r.x);
+  fe_shl(B, M, 3);          // 8M
+  fe_sub(r.x, t, B);        // X3 = F - 8M
+  fe_shl(M, M, 2);          // D = 4M
+  fe_sub(t, M, r.x);
   fe_mul(t, E, t);
-  fe_mul_small(C, C, 8);
+  fe_shl(C, C, 3);
   fe_sub(r.y, t, C);        // Y3 = E(D - X3) - 8C
 }
 
@@ -86,8 +86,8 @@ HKV_DEV void gej_add_ge_core(gej& r, const gej& a, const fe& az, const fe& bx, c
   if (zr) *zr = h;
   fe_sqr(t, rr);
   fe_sub(t, t, hhh);
-  fe_sub(t, t, v);
-  fe_sub(t, t, v);          // X3 = R^2 - H^3 - 2V
+  fe_shl(u2, v, 1);
+  fe_sub(t, t, u2);         // X3 = R^2 - H^3 - 2V
   fe_sub(v, v, t);
   fe_mul(v, rr, v);
   fe_mul(hhh, a.y, hhh);

@@ -157,7 +157,7 @@ HKV_DEV void shr_bits(uint32_t* a, int b) {
 // [pos-1, pos+W-1]; sum_w d_w 16^w reproduces the scalar (< 2^131).
 HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2,
                           uint32_t* SL, uint32_t* SH) {
-  uint32_t p1 = 0, p2 = 0, pl = 0, ph = 0;
+  uint32_t p1 = 0, p2 = 0;
 #pragma unroll 1
   for (int w = 0; w < NWIN; ++w) {
     const uint32_t v1 = p1 | ((S1[0] & 15u) << 1), v2 = p2 | ((S2[0] & 15u) << 1);
@@ -167,18 +167,20 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
     shr_bits<5>(S2, 4);
     const int d1 = (int)((v1 + 1u) >> 1) - (int)((v1 >> 4) << 4);
     const int d2 = (int)((v2 + 1u) >> 1) - (int)((v2 >> 4) << 4);
-    int dl = 0, dh = 0;
-    if ((w & 1) == 0) {
-      const uint32_t vl = pl | ((SL[0] & 255u) << 1), vh = ph | ((SH[0] & 255u) << 1);
-      pl = (SL[0] >> 7) & 1u;
-      ph = (SH[0] >> 7) & 1u;
-      shr_bits<4>(SL, 8);
-      shr_bits<4>(SH, 8);
-      dl = (int)((vl + 1u) >> 1) - (int)((vl >> 8) << 8);
-      dh = (int)((vh + 1u) >> 1) - (int)((vh >> 8) << 8);
-    }
-    im[(size_t)(IM_DIG + w) * n_pad + i] = (uint32_t)(d1 + 8) | ((uint32_t)(d2 + 8) << 5) |
-                                           ((uint32_t)(dl + 128) << 10) | ((uint32_t)(dh + 128) << 19);
+    im[(size_t)(IM_DIG + w) * n_pad + i] = (uint32_t)(d1 + 8) | ((uint32_t)(d2 + 8) << 5);
+  }
+  uint32_t pl = 0, ph = 0;
+#pragma unroll 1
+  for (int j = 0; j < GWIN; ++j) {
+    const uint32_t vl = pl | ((SL[0] & 0xFFFFu) << 1), vh = ph | ((SH[0] & 0xFFFFu) << 1);
+    pl = (SL[0] >> 15) & 1u;
+    ph = (SH[0] >> 15) & 1u;
+    shr_bits<4>(SL, 16);
+    shr_bits<4>(SH, 16);
+    const int dl = (int)((vl + 1u) >> 1) - (int)((vl >> 16) << 16);
+    const int dh = (int)((vh + 1u) >> 1) - (int)((vh >> 16) << 16);
+    im[(size_t)(IM_GDIG + 2 * j) * n_pad + i] = (uint32_t)(dl < 0 ? -dl : dl) | (dl < 0 ? 0x10000u : 0u);
+    im[(size_t)(IM_GDIG + 2 * j + 1) * n_pad + i] = (uint32_t)(dh < 0 ? -dh : dh) | (dh < 0 ? 0x10000u : 0u);
   }
 }
 
@@ -259,13 +261,10 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits) {
-  __shared__ __attribute__((aligned(16))) uint32_t gl[GTAB_DWORDS];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(gtab);
-    uint4* dst = reinterpret_cast<uint4*>(gl);
-    for (int k = threadIdx.x; k < GTAB_DWORDS / 4; k += WG) dst[k] = src[k];
-  }
-  __syncthreads();
+  // per wave: two G-entry slots, each 4 quads x 64 lanes x 16 B (LDS-DMA target)
+  __shared__ __attribute__((aligned(16))) uint4 gpf[WG / 64][2][4][64];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ln = threadIdx.x & 63;
 
   const uint32_t n_lanes = gridDim.x * WG;
   const uint32_t lane = blockIdx.x * WG + threadIdx.x;
@@ -366,6 +365,21 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         qtab_load(qs, n_lanes, lane, i2 * QTAB_QUADS_PER_ENTRY + 2, t2y);
       }
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
+      const bool gwin = (win & 3) == 0;
+      uint32_t gd0 = 0, gd1 = 0;
+      if (gwin) {
+        const int gj = win >> 2;
+        gd0 = valid ? im[(size_t)(IM_GDIG + 2 * gj) * n_pad + i] : 0u;
+        gd1 = valid ? im[(size_t)(IM_GDIG + 2 * gj + 1) * n_pad + i] : 0u;
+        const uint32_t m0 = gd0 & 0xFFFFu, m1 = gd1 & 0xFFFFu;
+        const uint4* e0 = reinterpret_cast<const uint4*>(gtab) + (size_t)(m0 ? m0 - 1 : 0) * 4;
+        const uint4* e1 = reinterpret_cast<const uint4*>(gtab) + ((size_t)GTAB_ENTRIES + (m1 ? m1 - 1 : 0)) * 4;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          __builtin_amdgcn_global_load_lds(e0 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][0][qd][0], 16, 0, 0);
+          __builtin_amdgcn_global_load_lds(e1 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][1][qd][0], 16, 0, 0);
+        }
+      }
       if (win != NWIN - 1) {
 #pragma unroll 1
         for (int d = 0; d < 4; ++d) gej_double(acc, acc);
@@ -387,18 +401,17 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         fe_cmov(ty, nty, neg);
         gej_accumulate(acc, inf, acc.z, tx, ty, tx, ty, take);
       }
-      // G terms every other window: slot 0 = u1_lo * G, slot 1 = u1_hi * 2^128 G
-      if ((win & 1) == 0) {
+      // G terms every fourth window (radix 2^16): slot 0 = u1_lo * G,
+      // slot 1 = u1_hi * 2^128 G; entries were DMA'd into LDS before the doublings.
+      if (gwin) {
 #pragma unroll 1
         for (int slot = 0; slot < 2; ++slot) {
-          const int dg = (int)((dw >> (slot == 0 ? 10 : 19)) & 511u) - 128;
-          const bool take = dg != 0;
-          const int mag = dg < 0 ? -dg : dg;
-          const int idx = take ? mag - 1 : 0;
-          const uint4* e = reinterpret_cast<const uint4*>(gl + (slot * GTAB_ENTRIES + idx) * 16);
+          const uint32_t gd = slot == 0 ? gd0 : gd1;
+          const bool take = (gd & 0xFFFFu) != 0;
           fe tx, ty;
           {
-            const uint4 a0 = e[0], a1 = e[1], a2 = e[2], a3 = e[3];
+            const uint4 a0 = gpf[wv][slot][0][ln], a1 = gpf[wv][slot][1][ln];
+            const uint4 a2 = gpf[wv][slot][2][ln], a3 = gpf[wv][slot][3][ln];
             tx.v[0] = a0.x; tx.v[1] = a0.y; tx.v[2] = a0.z; tx.v[3] = a0.w;
             tx.v[4] = a1.x; tx.v[5] = a1.y; tx.v[6] = a1.z; tx.v[7] = a1.w;
             ty.v[0] = a2.x; ty.v[1] = a2.y; ty.v[2] = a2.z; ty.v[3] = a2.w;
@@ -406,7 +419,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
           }
           fe nty;
           fe_neg(nty, ty);
-          fe_cmov(ty, nty, dg < 0);
+          fe_cmov(ty, nty, (gd & 0x10000u) != 0);
           fe az;
           fe_mul(az, acc.z, Zg);
           fe itx = tx, ity = ty;

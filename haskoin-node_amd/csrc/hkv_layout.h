@@ -19,30 +19,33 @@ enum : int {
   IM_U1H = 31,    // 4 limbs, u1 bits 128..255
   IM_R = 35,      // 8 limbs, r (< n)
   IM_C = 43,      // 8 limbs, batch-inversion prefix product (scalar kernel scratch)
-  IM_DIG = 51,    // 33 words: window w's Booth digits (see DIG_* below)
-  IM_WORDS = 84,
+  IM_DIG = 51,    // 33 words: window w's radix-16 Booth digits of k1, k2
+  IM_GDIG = 84,   // 2 x 9 words: radix-2^16 Booth digits of u1_lo, u1_hi
+  IM_WORDS = 102,
   // between the parse and scalar kernels: s (normalised) and m = msg mod n
   IM_S = IM_K1,   // 8 limbs over K1|K2 (10 words)
   IM_M = IM_U1L,  // 8 limbs over U1L|U1H
 };
-// Digit word of window w (w = 0..32, bit position 4w): biased Booth digits
-//   bits 0-4   d1 + 8    (k1, radix 16, -8..8)
-//   bits 5-9   d2 + 8    (k2, radix 16)
-//   bits 10-18 dl + 128  (u1 bits 0..127, radix 256, even w only, else 0)
-//   bits 19-27 dh + 128  (u1 bits 128..255, radix 256, even w only)
+// Q digit word of window w (w = 0..32, bit position 4w): biased Booth digits
+//   bits 0-4 d1 + 8 (k1, radix 16, -8..8), bits 5-9 d2 + 8 (k2)
+// G digit word of G window j (j = 0..8, bit position 16j = Q window 4j),
+// one per u1 half: bits 0-15 |d| (0..32768), bit 16 sign.
 constexpr int NWIN = 33;
-constexpr uint32_t DIG_ZERO = 8u | (8u << 5) | (128u << 10) | (128u << 19);
+constexpr int GWIN = 9;
+constexpr uint32_t DIG_ZERO = 8u | (8u << 5);
 
 // signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
 // Montgomery's trick: 3(B-1) multiplications + 1 inversion)
 constexpr int BATCH_INV = 8;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
-// Fixed-base tables: odd/even multiples j*B for j = 1..128, B in {G, 2^128 G},
-// affine, 16 dwords per entry [x(8) | y(8)], table t at entry offset t*128.
-constexpr int GTAB_W = 8;              // Booth radix 2^8
-constexpr int GTAB_ENTRIES = 128;
-constexpr int GTAB_DWORDS = 2 * GTAB_ENTRIES * 16;
+// Fixed-base tables in HBM (4 MiB, L2/MALL resident): multiples j*B for
+// j = 1..32768, B in {G, 2^128 G}, affine, 16 dwords per entry
+// [x(8) | y(8)], table t at entry offset t*32768. Gathered per lane by
+// LDS-DMA one window ahead of use.
+constexpr int GTAB_W = 16;             // Booth radix 2^16
+constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
+constexpr size_t GTAB_DWORDS = 2ull * GTAB_ENTRIES * 16;
 
 // Per-lane Q table: multiples j*Q, j = 1..8, affine on the lane's isomorphic
 // curve; per entry 6 quads (16 B): x(2) | y(2) | beta*x(2). Quad q of lane L

@@ -20,15 +20,16 @@ SC_RED = 8 * 4 + 5 * 4 + 4   # three folds by NC's low 128 bits
 SC_MUL = MUL256 + SC_RED
 SC_SQR = SQR256 + SC_RED
 
-GEJ_DOUBLE = 2 * FE_MUL + 5 * FE_SQR + 2 * FE_MUL_SMALL       # dbl-2009-l
+GEJ_DOUBLE = 3 * FE_MUL + 4 * FE_SQR + FE_MUL_SMALL           # a=0, D = 4XB; 2^k scalings are shifts
 GEJ_ADD_GE = 8 * FE_MUL + 3 * FE_SQR                          # mixed add
 GEJ_ADD_ZINV = GEJ_ADD_GE + FE_MUL                            # + az = Z*Zg
 
 Q_WINDOWS = 33       # radix-16 Booth over 132 bits
-G_WINDOWS = 17       # radix-256 Booth over 136 bits
+G_WINDOWS = 9        # radix-2^16 Booth over 144 bits (u1 halves)
 DOUBLINGS = 4 * (Q_WINDOWS - 1)
 
 SC_INV_LOW = 0x0BAAEDCE6AF48A03BBFD25E8CD036413F
+BATCH_INV = 8        # signatures per s^-1 (hkv_layout.h)
 
 
 def ecmult_products() -> int:
@@ -50,8 +51,10 @@ def prologue_products() -> int:
     curve = FE_SQR + FE_MUL + FE_SQR                 # x^3 + 7, y^2 check
     x127 = (1 + 1 + 3 + 6 + 12 + 24 + 48 + 24 + 6 + 1) * SC_SQR + 10 * SC_MUL
     inv = x127 + 129 * SC_SQR + bin(SC_INV_LOW).count("1") * SC_MUL
+    batch = BATCH_INV
+    inv_per_sig = (inv + 3 * (batch - 1) * SC_MUL) // batch   # Montgomery's trick
     glv = 2 * MUL256 + 3 * SC_MUL
-    return sqrt + curve + inv + 2 * SC_MUL + glv
+    return sqrt + curve + inv_per_sig + 2 * SC_MUL + glv
 
 
 ECMULT_PRODUCTS_PER_VERIFY = ecmult_products()
