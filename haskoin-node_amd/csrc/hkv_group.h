@@ -96,31 +96,59 @@ HKV_DEV void gej_add_ge_core(gej& r, const gej& a, const fe& az, const fe& bx, c
 }
 
 // Complete "accumulate" step used by every ecmult loop:
-//   acc (+inf flag) += T  where T = (tx, ty) affine (scale az as above),
-//   `take` = this lane adds (digit != 0). Handles acc = inf, acc = T (double),
-//   acc = -T (infinity) exactly. inf_init = (tx, ty, 1) is what acc becomes
-//   when it was infinity (caller supplies it already mapped to acc's curve).
-HKV_DEV void gej_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, const fe& ty,
-                            const fe& itx, const fe& ity, bool take) {
-  gej s;
-  bool hz, rz;
-  gej_add_ge_core(s, acc, az, tx, ty, hz, rz, nullptr);
-  const bool degenerate = take && !inf && hz;
-  if (__builtin_expect(__any(degenerate), 0)) {
-    gej d;
-    gej_double(d, acc);
-    gej_cmov(s, d, rz);
+//   acc (+inf flag) += T  where T = (tx, ty) is affine on the curve of
+//   Jacobian scale az (see gej_add_ge_core), `take` = this lane adds
+//   (digit != 0). Lanes whose acc is infinity are left to the caller
+//   (gej_accumulate_from_inf), so the mapped init point is only built when
+//   some lane needs it.
+// H = U2 - X1 is tested before anything is written, so the sum (8M + 3S) is
+// computed in place under the lane mask live && H != 0: lanes that do not
+// add keep their point without a copy, and acc = +-T (H == 0, rare) is then
+// resolved exactly by a masked doubling or by going to infinity.
+HKV_DEV void gej_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, const fe& ty, bool take) {
+  fe h, rr;
+  {
+    fe z2, t;
+    fe_sqr(z2, az);
+    fe_mul(h, tx, z2);        // U2
+    fe_mul(t, az, z2);
+    fe_mul(rr, ty, t);        // S2
   }
-  // new state
-  const bool to_inf = take && !inf && hz && !rz;
-  const bool from_inf = take && inf;
-  gej_cmov(acc, s, take && !inf && !(hz && !rz));
-  if (from_inf) {
-    acc.x = itx;
-    acc.y = ity;
-    fe_set_u32(acc.z, 1);
+  fe_sub(h, h, acc.x);        // H = U2 - X1
+  fe_sub(rr, rr, acc.y);      // R = S2 - Y1
+  const bool live = take && !inf;
+  const bool hz = fe_is_zero(h);
+  if (live && !hz) {
+    fe hh, hhh, t2;
+    fe_sqr(hh, h);
+    fe_mul(hhh, h, hh);       // H^3
+    fe_mul(hh, acc.x, hh);    // V = X1 H^2
+    fe_mul(acc.z, acc.z, h);  // Z3 = Z1 H
+    fe_sqr(h, rr);
+    fe_sub(h, h, hhh);
+    fe_shl(t2, hh, 1);
+    fe_sub(acc.x, h, t2);     // X3 = R^2 - H^3 - 2V
+    fe_sub(hh, hh, acc.x);
+    fe_mul(hh, rr, hh);
+    fe_mul(hhh, acc.y, hhh);
+    fe_sub(acc.y, hh, hhh);   // Y3 = R(V - X3) - Y1 H^3
   }
-  inf = (inf && !take) || to_inf;
+  const bool degen = live && hz;
+  if (__builtin_expect(__any(degen), 0)) {
+    const bool rz = fe_is_zero(rr);
+    if (degen && rz) gej_double(acc, acc);   // T == acc
+    inf = inf || (degen && !rz);             // T == -acc
+  }
+}
+// acc := (itx, ity, 1) on lanes that take a point while at infinity
+HKV_DEV void gej_accumulate_from_inf(gej& acc, bool& inf, const fe& itx, const fe& ity, bool take) {
+  const bool f = take && inf;
+  fe_cmov(acc.x, itx, f);
+  fe_cmov(acc.y, ity, f);
+  fe one;
+  fe_set_u32(one, 1);
+  fe_cmov(acc.z, one, f);
+  inf = inf && !take;
 }
 
 }  // namespace hkv

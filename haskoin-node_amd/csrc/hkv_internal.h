@@ -19,6 +19,7 @@ enum {
   HKV_DBG_GLV = 9,
   HKV_DBG_ECMULT_G = 10,
   HKV_DBG_MUL512 = 11,
+  HKV_DBG_SQR512 = 12,
 };
 
 namespace hkv {

@@ -46,7 +46,7 @@ __constant__ static const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC
 // ---------------------------------------------------------------------------
 // 1. prologue
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(WG) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
+__global__ void __launch_bounds__(WG, 4) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
                                                           uint32_t n_pad, uint32_t mode,
                                                           uint32_t* __restrict__ im) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
@@ -355,15 +355,8 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
 #pragma unroll 1
     for (int win = NWIN - 1; win >= 0; --win) {
       const int d1 = (int)(dw & 31u) - 8, d2 = (int)((dw >> 5) & 31u) - 8;
-      fe t1x, t1y, t2x, t2y;
-      {
-        const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
-        const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
-        qtab_load(qs, n_lanes, lane, i1 * QTAB_QUADS_PER_ENTRY + 0, t1x);
-        qtab_load(qs, n_lanes, lane, i1 * QTAB_QUADS_PER_ENTRY + 2, t1y);
-        qtab_load(qs, n_lanes, lane, i2 * QTAB_QUADS_PER_ENTRY + 4, t2x);
-        qtab_load(qs, n_lanes, lane, i2 * QTAB_QUADS_PER_ENTRY + 2, t2y);
-      }
+      const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
+      const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
       const bool gwin = (win & 3) == 0;
       uint32_t gd0 = 0, gd1 = 0;
@@ -382,7 +375,9 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       }
       if (win != NWIN - 1) {
 #pragma unroll 1
-        for (int d = 0; d < 4; ++d) gej_double(acc, acc);
+        for (int d = 0; d < 4; ++d) {
+          if (!inf) gej_double(acc, acc);
+        }
       }
       // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
 #pragma unroll 1
@@ -391,15 +386,14 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         const bool take = dg != 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
         fe tx, ty;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          tx.v[k] = slot == 0 ? t1x.v[k] : t2x.v[k];
-          ty.v[k] = slot == 0 ? t1y.v[k] : t2y.v[k];
-        }
+        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2) * QTAB_QUADS_PER_ENTRY + (slot == 0 ? 0 : 4), tx);
+        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2) * QTAB_QUADS_PER_ENTRY + 2, ty);
         fe nty;
         fe_neg(nty, ty);
         fe_cmov(ty, nty, neg);
-        gej_accumulate(acc, inf, acc.z, tx, ty, tx, ty, take);
+        const bool was_inf = inf;
+        gej_accumulate(acc, inf, acc.z, tx, ty, take);
+        gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
       }
       // G terms every fourth window (radix 2^16): slot 0 = u1_lo * G,
       // slot 1 = u1_hi * 2^128 G; entries were DMA'd into LDS before the doublings.
@@ -422,15 +416,16 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
           fe_cmov(ty, nty, (gd & 0x10000u) != 0);
           fe az;
           fe_mul(az, acc.z, Zg);
-          fe itx = tx, ity = ty;
-          if (__any(take && inf)) {  // map G-multiple onto the accumulator's curve
-            fe zg2, zg3;
+          const bool was_inf = inf;
+          gej_accumulate(acc, inf, az, tx, ty, take);
+          if (__any(take && was_inf)) {  // map the G-multiple onto the accumulator's curve
+            fe zg2;
             fe_sqr(zg2, Zg);
-            fe_mul(zg3, zg2, Zg);
-            fe_mul(itx, tx, zg2);
-            fe_mul(ity, ty, zg3);
+            fe_mul(tx, tx, zg2);
+            fe_mul(zg2, zg2, Zg);
+            fe_mul(ty, ty, zg2);
+            gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
           }
-          gej_accumulate(acc, inf, az, tx, ty, itx, ity, take);
         }
       }
       dw = dw_next;
@@ -478,7 +473,9 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
 // with complete additions (slow, used off the timed path only).
 // ---------------------------------------------------------------------------
 HKV_DEV void gej_add_affine_complete(gej& acc, bool& inf, const ge& b, bool take) {
-  gej_accumulate(acc, inf, acc.z, b.x, b.y, b.x, b.y, take);
+  const bool was_inf = inf;
+  gej_accumulate(acc, inf, acc.z, b.x, b.y, take);
+  gej_accumulate_from_inf(acc, inf, b.x, b.y, take && was_inf);
 }
 // r = a*G + b*P (either scalar may be zero), affine output; returns false if infinity
 HKV_DEV bool ecmult_simple(ge& out, const sc& a, const sc& b, const ge& p) {
@@ -677,6 +674,7 @@ __global__ void __launch_bounds__(WG) hkv_debug_kernel(uint32_t op, uint32_t n, 
       break;
     }
     case HKV_DBG_MUL512: mul512(res, x.v, y.v); break;
+    case HKV_DBG_SQR512: sqr512(res, x.v); break;
     default: break;
   }
 #pragma unroll

@@ -58,7 +58,7 @@ constexpr int WG = 256;                // threads per workgroup (4 waves)
 
 // minimum waves per SIMD the ecmult kernel's register allocation targets
 #ifndef HKV_ECMULT_WAVES
-#define HKV_ECMULT_WAVES 2
+#define HKV_ECMULT_WAVES 4
 #endif
 
 }  // namespace hkv

@@ -130,7 +130,7 @@ HKV_DEV void sc_mul(sc& r, const sc& a, const sc& b) {
 }
 HKV_DEV void sc_sqr(sc& r, const sc& a) {
   uint32_t t[16];
-  sqr256(t, a.v);
+  sqr512(t, a.v);
   sc_reduce512(r, t);
 }
 HKV_DEV void sc_add(sc& r, const sc& a, const sc& b) {

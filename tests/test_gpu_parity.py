@@ -13,7 +13,7 @@ from conftest import oracle_batch
 pytestmark = pytest.mark.gpu
 
 HKV_DBG = dict(FE_MUL=1, FE_SQR=2, FE_ADD=3, FE_SUB=4, FE_INV=5, FE_SQRT=6, SC_MUL=7, SC_INV=8, GLV=9,
-               ECMULT_G=10, MUL512=11)
+               ECMULT_G=10, MUL512=11, SQR512=12)
 
 
 @pytest.fixture(scope="module")
@@ -80,6 +80,9 @@ def test_mul512_product(torch, ver):
     out = run_debug(torch, ver, "MUL512", xs, ys)
     for i in range(len(xs)):
         assert from_limbs(list(out[i, :8])) + (from_limbs(list(out[i, 8:16])) << 256) == xs[i] * ys[i]
+    out = run_debug(torch, ver, "SQR512", xs, ys)
+    for i in range(len(xs)):
+        assert from_limbs(list(out[i, :8])) + (from_limbs(list(out[i, 8:16])) << 256) == xs[i] * xs[i]
 
 
 def test_field_inv_sqrt(torch, ver):
