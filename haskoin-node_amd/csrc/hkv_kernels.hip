@@ -184,7 +184,7 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
   }
 }
 
-__global__ void __launch_bounds__(WG) hkv_scalar_kernel(uint32_t n_pad, uint32_t stride, uint32_t* __restrict__ im) {
+__global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t stride, uint32_t* __restrict__ im) {
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
   if (t >= stride) return;
   // forward: prefix products c_k = s_0 * ... * s_k (invalid lanes use s = 1)
@@ -203,13 +203,12 @@ __global__ void __launch_bounds__(WG) hkv_scalar_kernel(uint32_t n_pad, uint32_t
   }
   sc inv;
   sc_inv(inv, c);
-  // backward: s_k^-1 = inv * c_{k-1}; inv *= s_k
+  // backward: s_k^-1 = inv * c_{k-1} (stored over c_k); inv *= s_k
 #pragma unroll 1
   for (int k = BATCH_INV - 1; k >= 0; --k) {
     const uint32_t i = t + (uint32_t)k * stride;
     if (i >= n_pad) continue;
-    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-    const bool valid = (flags & FLAG_VALID) != 0;
+    const bool valid = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_VALID) != 0;
     sc prev, sv, sinv;
     if (k > 0) {
       im_load8(im, n_pad, IM_C, i - stride, prev.v);
@@ -217,28 +216,37 @@ __global__ void __launch_bounds__(WG) hkv_scalar_kernel(uint32_t n_pad, uint32_t
       sc_set_u32(prev, 1);
     }
     sc_mul(sinv, inv, prev);
+    im_store8(im, n_pad, IM_C, i, sinv.v);
     im_load8(im, n_pad, IM_S, i, sv.v);
     if (!valid) sc_set_u32(sv, 1);
     sc_mul(inv, inv, sv);
-    sc m, r, u1, u2;
-    im_load8(im, n_pad, IM_M, i, m.v);
-    im_load8(im, n_pad, IM_R, i, r.v);
-    sc_mul(u1, m, sinv);
-    sc_mul(u2, r, sinv);
-    uint32_t k1[5], k2[5];
-    bool n1, n2;
-    const bool glv_ok = glv_split(u2, k1, n1, k2, n2);
-    uint32_t f = flags | (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
-    if (!glv_ok) f &= ~FLAG_VALID;  // unreachable for a correct basis; fail closed
-    im[(size_t)IM_FLAGS * n_pad + i] = f;
-    const bool use = (f & FLAG_VALID) != 0;
-    uint32_t S1[5], S2[5], SL[4], SH[4];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
-    write_digits(im, n_pad, i, S1, S2, SL, SH);
   }
+}
+
+// 1c. per signature: u1 = m/s, u2 = r/s, GLV split of u2, Booth digits.
+__global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* __restrict__ im) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  sc sinv, m, r, u1, u2;
+  im_load8(im, n_pad, IM_C, i, sinv.v);
+  im_load8(im, n_pad, IM_M, i, m.v);
+  im_load8(im, n_pad, IM_R, i, r.v);
+  sc_mul(u1, m, sinv);
+  sc_mul(u2, r, sinv);
+  uint32_t k1[5], k2[5];
+  bool n1, n2;
+  const bool glv_ok = glv_split(u2, k1, n1, k2, n2);
+  uint32_t f = flags | (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
+  if (!glv_ok) f &= ~FLAG_VALID;  // unreachable for a correct basis; fail closed
+  im[(size_t)IM_FLAGS * n_pad + i] = f;
+  const bool use = (f & FLAG_VALID) != 0;
+  uint32_t S1[5], S2[5], SL[4], SH[4];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
+  write_digits(im, n_pad, i, S1, S2, SL, SH);
 }
 
 // ---------------------------------------------------------------------------
@@ -697,7 +705,10 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t stride = ceil_div(n_pad, BATCH_INV);
-  hipLaunchKernelGGL(hkv_scalar_kernel, dim3(ceil_div(stride, WG)), dim3(WG), 0, st, n_pad, stride, im);
+  hipLaunchKernelGGL(hkv_inv_kernel, dim3(ceil_div(stride, WG)), dim3(WG), 0, st, n_pad, stride, im);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,

@@ -18,7 +18,7 @@ enum : int {
   IM_U1L = 27,    // 4 limbs, u1 bits 0..127
   IM_U1H = 31,    // 4 limbs, u1 bits 128..255
   IM_R = 35,      // 8 limbs, r (< n)
-  IM_C = 43,      // 8 limbs, batch-inversion prefix product (scalar kernel scratch)
+  IM_C = 43,      // 8 limbs, batch-inversion prefix product, then s^-1
   IM_DIG = 51,    // 33 words: window w's radix-16 Booth digits of k1, k2
   IM_GDIG = 84,   // 2 x 9 words: radix-2^16 Booth digits of u1_lo, u1_hi
   IM_WORDS = 102,
@@ -36,7 +36,7 @@ constexpr uint32_t DIG_ZERO = 8u | (8u << 5);
 
 // signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
 // Montgomery's trick: 3(B-1) multiplications + 1 inversion)
-constexpr int BATCH_INV = 8;
+constexpr int BATCH_INV = 16;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
 // Fixed-base tables in HBM (4 MiB, L2/MALL resident): multiples j*B for

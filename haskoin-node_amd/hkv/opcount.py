@@ -29,7 +29,7 @@ G_WINDOWS = 9        # radix-2^16 Booth over 144 bits (u1 halves)
 DOUBLINGS = 4 * (Q_WINDOWS - 1)
 
 SC_INV_LOW = 0x0BAAEDCE6AF48A03BBFD25E8CD036413F
-BATCH_INV = 8        # signatures per s^-1 (hkv_layout.h)
+BATCH_INV = 16       # signatures per s^-1 (hkv_layout.h)
 
 
 def ecmult_products() -> int:
