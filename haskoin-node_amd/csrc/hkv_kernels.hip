@@ -252,15 +252,21 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 // ---------------------------------------------------------------------------
 // 2. ecmult + x compare
 // ---------------------------------------------------------------------------
-HKV_DEV void qtab_store(uint32_t* __restrict__ qs, uint32_t n_lanes, uint32_t lane, int quad, const fe& a) {
-  uint4* p0 = reinterpret_cast<uint4*>(qs) + (size_t)quad * n_lanes + lane;
-  uint4* p1 = reinterpret_cast<uint4*>(qs) + (size_t)(quad + 1) * n_lanes + lane;
-  *p0 = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
-  *p1 = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+// Per-lane Q table, entry-major then lane: entry e of lane L is 96 contiguous
+// bytes (quads x0 x1 | y0 y1 | bx0 bx1) at quad offset (e * n_lanes + L) * 6,
+// so a lookup reads 64 contiguous bytes per lane (half a 128-B line) whatever
+// entry the neighbouring lanes pick.
+HKV_DEV uint4* qtab_ptr(uint32_t* qs, uint32_t n_lanes, uint32_t lane, int entry, int c) {
+  return reinterpret_cast<uint4*>(qs) + ((size_t)entry * n_lanes + lane) * QTAB_QUADS_PER_ENTRY + c;
 }
-HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32_t lane, int quad, fe& a) {
-  const uint4 v0 = reinterpret_cast<const uint4*>(qs)[(size_t)quad * n_lanes + lane];
-  const uint4 v1 = reinterpret_cast<const uint4*>(qs)[(size_t)(quad + 1) * n_lanes + lane];
+HKV_DEV void qtab_store(uint32_t* __restrict__ qs, uint32_t n_lanes, uint32_t lane, int entry, int c, const fe& a) {
+  uint4* p = qtab_ptr(qs, n_lanes, lane, entry, c);
+  p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  p[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32_t lane, int entry, int c, fe& a) {
+  const uint4* p = qtab_ptr(const_cast<uint32_t*>(qs), n_lanes, lane, entry, c);
+  const uint4 v0 = p[0], v1 = p[1];
   a.v[0] = v0.x; a.v[1] = v0.y; a.v[2] = v0.z; a.v[3] = v0.w;
   a.v[4] = v1.x; a.v[5] = v1.y; a.v[6] = v1.z; a.v[7] = v1.w;
 }
@@ -304,10 +310,10 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       fe_mul(qx, q.x, z2);
       fe_mul(z2, z2, p2.z);
       fe_mul(qy, q.y, z2);
-      qtab_store(qs, n_lanes, lane, 0 * QTAB_QUADS_PER_ENTRY + 0, qx);
-      qtab_store(qs, n_lanes, lane, 0 * QTAB_QUADS_PER_ENTRY + 2, qy);
-      qtab_store(qs, n_lanes, lane, 1 * QTAB_QUADS_PER_ENTRY + 0, p2.x);
-      qtab_store(qs, n_lanes, lane, 1 * QTAB_QUADS_PER_ENTRY + 2, p2.y);
+      qtab_store(qs, n_lanes, lane, 0, 0, qx);
+      qtab_store(qs, n_lanes, lane, 0, 2, qy);
+      qtab_store(qs, n_lanes, lane, 1, 0, p2.x);
+      qtab_store(qs, n_lanes, lane, 1, 2, p2.y);
       pj.x = p2.x;
       pj.y = p2.y;
       fe_set_u32(pj.z, 1);
@@ -316,9 +322,9 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         bool hz, rz;
         fe h;
         gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
-        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 0, pj.x);
-        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 2, pj.y);
-        qtab_store(qs, n_lanes, lane, (j - 1) * QTAB_QUADS_PER_ENTRY + 4, h);
+        qtab_store(qs, n_lanes, lane, j, 0, pj.x);
+        qtab_store(qs, n_lanes, lane, j, 2, pj.y);
+        qtab_store(qs, n_lanes, lane, (j - 1), 4, h);
       }
       fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
       fe beta;
@@ -327,7 +333,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       {
         fe bx;
         fe_mul(bx, pj.x, beta);
-        qtab_store(qs, n_lanes, lane, 7 * QTAB_QUADS_PER_ENTRY + 4, bx);
+        qtab_store(qs, n_lanes, lane, 7, 4, bx);
       }
       fe rho;
       fe_set_u32(rho, 1);
@@ -335,19 +341,19 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       for (int j = 6; j >= 0; --j) {
         fe x, y, t;
         if (j >= 1) {
-          qtab_load(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 4, t);  // H_{j+1}
+          qtab_load(qs, n_lanes, lane, j, 4, t);  // H_{j+1}
           fe_mul(rho, rho, t);
         }
-        qtab_load(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 0, x);
-        qtab_load(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 2, y);
+        qtab_load(qs, n_lanes, lane, j, 0, x);
+        qtab_load(qs, n_lanes, lane, j, 2, y);
         fe_sqr(t, rho);
         fe_mul(x, x, t);
         fe_mul(t, t, rho);
         fe_mul(y, y, t);
-        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 0, x);
-        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 2, y);
+        qtab_store(qs, n_lanes, lane, j, 0, x);
+        qtab_store(qs, n_lanes, lane, j, 2, y);
         fe_mul(x, x, beta);
-        qtab_store(qs, n_lanes, lane, j * QTAB_QUADS_PER_ENTRY + 4, x);
+        qtab_store(qs, n_lanes, lane, j, 4, x);
       }
     }
 
@@ -394,8 +400,8 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         const bool take = dg != 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
         fe tx, ty;
-        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2) * QTAB_QUADS_PER_ENTRY + (slot == 0 ? 0 : 4), tx);
-        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2) * QTAB_QUADS_PER_ENTRY + 2, ty);
+        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
+        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
         fe nty;
         fe_neg(nty, ty);
         fe_cmov(ty, nty, neg);

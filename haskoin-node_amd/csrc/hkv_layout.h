@@ -48,8 +48,8 @@ constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
 constexpr size_t GTAB_DWORDS = 2ull * GTAB_ENTRIES * 16;
 
 // Per-lane Q table: multiples j*Q, j = 1..8, affine on the lane's isomorphic
-// curve; per entry 6 quads (16 B): x(2) | y(2) | beta*x(2). Quad q of lane L
-// at [(q * n_lanes + L) * 4] dwords (lane-contiguous, coalesced stores).
+// curve; per entry 6 quads (16 B): x(2) | y(2) | beta*x(2); entry e of lane L
+// at quad (e * n_lanes + L) * 6 (hkv_kernels.hip qtab_ptr).
 constexpr int QTAB_ENTRIES = 8;
 constexpr int QTAB_QUADS_PER_ENTRY = 6;
 constexpr int QTAB_QUADS = QTAB_ENTRIES * QTAB_QUADS_PER_ENTRY;

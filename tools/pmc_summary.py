@@ -1,0 +1,53 @@
+"""Summarise a tools/profile_round.sh output directory into profiles/.
+
+    python tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<tag>
+
+Writes <dest>/kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
+<dest>/pmc.json (per-kernel counters of the 1M-record bench dispatches) and
+profiles/latest_pmc_traffic.json, which bench.py reads for roofline.traffic:
+HBM-side bytes per ecmult launch = (FETCH_SIZE + WRITE_SIZE) * 1024, from
+separate --pmc passes (MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KB
+counted at the L2 memory side; Infinity-Cache hits are included; the 1/2
+read-side correction is documented for 16-B/lane streaming reads only, so the
+gather traffic here is reported uncorrected).
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def main(src: str, dst: str) -> None:
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    per = defaultdict(lambda: defaultdict(list))
+    grid = {}
+    for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            g = int(r["Grid_Size"])
+            k = r["Kernel_Name"].split("(")[0].replace("hkv::", "")
+            if g < 65536 or not k.startswith("hkv_"):
+                continue
+            per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            grid[k] = g
+    out = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in per.items()}
+    for k in out:
+        out[k]["Grid_Size"] = grid[k]
+    json.dump(out, open(os.path.join(dst, "pmc.json"), "w"), indent=1)
+    e = out.get("hkv_ecmult_kernel", {})
+    if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
+        t = {"kernel": "hkv_ecmult_kernel", "per_verify_records": 1 << 20,
+             "fetch_bytes_per_launch": e["FETCH_SIZE"] * 1024, "write_bytes_per_launch": e["WRITE_SIZE"] * 1024,
+             "hbm_bytes_per_launch": (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024,
+             "source": os.path.relpath(dst), "note": "uncorrected FETCH_SIZE+WRITE_SIZE (KB*1024), separate pmc passes"}
+        json.dump(t, open(os.path.join(os.path.dirname(dst.rstrip("/")), "latest_pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps({k: {c: "%.4g" % v for c, v in d.items()} for k, d in out.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
