@@ -1,0 +1,131 @@
+"""Seeded transaction / block generators for the sighash and standard-input
+tests (test infrastructure: builds inputs with the oracle's codec and signs
+with the oracle's curve arithmetic)."""
+from __future__ import annotations
+
+import random
+from typing import List, Optional, Tuple
+
+import secp256k1_oracle as o
+import sighash_oracle as sh
+
+
+def rand_script(rng: random.Random, n: int) -> bytes:
+    return bytes(rng.randrange(256) for _ in range(n))
+
+
+def rand_tx(rng: random.Random, nin: int, nout: int, segwit: bool = False, big_scripts: bool = False) -> sh.Tx:
+    ins = []
+    for _ in range(nin):
+        slen = rng.choice([0, 1, 25, 106, 107, 139]) if not big_scripts else rng.choice([0, 252, 253, 300, 70000])
+        ins.append(sh.TxIn(rand_script(rng, 32), rng.randrange(2**32), rand_script(rng, slen),
+                           rng.choice([0xFFFFFFFF, 0xFFFFFFFE, rng.randrange(2**32)])))
+    outs = []
+    for _ in range(nout):
+        slen = rng.choice([0, 22, 23, 25, 34, 80]) if not big_scripts else rng.choice([0, 252, 253, 1000])
+        outs.append(sh.TxOut(rng.randrange(2**64), rand_script(rng, slen)))
+    wit = []
+    if segwit:
+        for _ in range(nin):
+            wit.append([rand_script(rng, rng.choice([0, 33, 72])) for _ in range(rng.randrange(3))])
+        if not any(len(w) for w in wit):
+            wit[0] = [b"\x01"]
+    return sh.Tx(rng.choice([1, 2, 0xFFFFFFFF]), ins, outs, wit, rng.randrange(2**32))
+
+
+def rand_sighash(rng: random.Random) -> int:
+    return rng.choice([1, 1, 1, 2, 3, 0x81, 0x82, 0x83, 0x41, 0xC1, 0x43, 0, 4, 0x1F, 0x21, 0xFF,
+                       0x12345601, rng.randrange(2**32)])
+
+
+def rand_code(rng: random.Random) -> bytes:
+    kind = rng.randrange(6)
+    if kind == 0:
+        return sh.p2pkh_script(rand_script(rng, 20))
+    if kind == 1:   # with OP_CODESEPARATORs between ops
+        return b"\xab" + sh.p2pkh_script(rand_script(rng, 20))[:3] + rand_script(rng, 20) + b"\xab\x88\xac\xab"
+    if kind == 2:   # 0xab inside push data must survive
+        return b"\x05\xab\xab\xab\xab\xab\xab\x4c\x02\xab\x01\xab"
+    if kind == 3:   # truncated push: not a parseable script, kept verbatim
+        return b"\xab\x4c\xff\xab"
+    if kind == 4:
+        return b""
+    return rand_script(rng, rng.choice([1, 10, 300]))
+
+
+# --- signing (private keys; RFC6979 is not needed for tests) -----------------
+
+def sign(msg32: bytes, d: int, k: int) -> Tuple[int, int]:
+    R = o.point_mul(k, o.G)
+    r = R[0] % o.N
+    s = pow(k, -1, o.N) * (int.from_bytes(msg32, "big") + r * d) % o.N
+    if s > o.N // 2:
+        s = o.N - s
+    return r, s
+
+
+class Key:
+    def __init__(self, d: int, compressed: bool = True):
+        self.d = d
+        self.q = o.point_mul(d, o.G)
+        self.pub = o.pubkey_serialize(self.q, compressed)
+        self.h160 = sh.hash160(self.pub)
+
+
+def push(data: bytes) -> bytes:
+    n = len(data)
+    if n <= 75:
+        return bytes([n]) + data
+    if n <= 255:
+        return b"\x4c" + bytes([n]) + data
+    return b"\x4d" + n.to_bytes(2, "little") + data
+
+
+def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[int] = None,
+              p2wpkh_share: float = 0.6, p2pk_share: float = 0.0):
+    """A synthetic block mix: every tx spends 1-3 standard prevouts (P2WPKH /
+    P2PKH / P2PK) and pays 2 outputs, SIGHASH_ALL (| FORKID on a fork-id
+    network). Returns (txs, jobs) with jobs = [(tx index, input, prevout
+    script, value)]."""
+    txs, jobs = [], []
+    shbyte = 0x41 if forkid is not None else 0x01
+    for t in range(n_tx):
+        nin = rng.choice([1, 1, 2, 2, 3])
+        kinds, ks, vals = [], [], []
+        ins = []
+        for _ in range(nin):
+            u = rng.random()
+            kind = "p2wpkh" if u < p2wpkh_share else ("p2pk" if u < p2wpkh_share + p2pk_share else "p2pkh")
+            kinds.append(kind)
+            ks.append(rng.choice(keys))
+            vals.append(rng.randrange(1, 2**50))
+            ins.append(sh.TxIn(rand_script(rng, 32), rng.randrange(4), b"", 0xFFFFFFFF))
+        outs = [sh.TxOut(rng.randrange(1, 2**40), sh.p2pkh_script(rand_script(rng, 20))) for _ in range(2)]
+        tx = sh.Tx(rng.choice([1, 2]), ins, outs, [[] for _ in range(nin)], rng.randrange(600000))
+        prevs = []
+        for j in range(nin):
+            k = ks[j]
+            if kinds[j] == "p2wpkh":
+                prevs.append(sh.p2wpkh_script(k.h160))
+            elif kinds[j] == "p2pk":
+                prevs.append(push(k.pub) + b"\xac")
+            else:
+                prevs.append(sh.p2pkh_script(k.h160))
+        for j in range(nin):
+            k = ks[j]
+            if kinds[j] == "p2wpkh":
+                m = sh.sighash_forkid(tx, sh.p2pkh_script(k.h160), vals[j], j, shbyte, forkid)
+            else:
+                m = sh.sighash_legacy(tx, prevs[j], vals[j], j, shbyte, forkid)
+            r, s = sign(m, k.d, rng.randrange(1, o.N))
+            sig = sh.der_encode(r, s) + bytes([shbyte])
+            if kinds[j] == "p2wpkh":
+                tx.witness[j] = [sig, k.pub]
+            elif kinds[j] == "p2pk":
+                tx.inputs[j].script = push(sig)
+            else:
+                tx.inputs[j].script = push(sig) + push(k.pub)
+        txs.append(tx)
+        for j in range(nin):
+            jobs.append((t, j, prevs[j], vals[j]))
+    return txs, jobs
