@@ -41,6 +41,11 @@ struct DevCtx {
   uint32_t* pool = nullptr;
   uint32_t pool_n = 0;
   uint64_t pool_seed = ~0ull;
+  // tx index rows (hkv_sighash.hip) and host-API staging buffers
+  uint32_t* txt = nullptr;
+  size_t txt_cap = 0;  // bytes
+  void* stage[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t stage_cap[5] = {0, 0, 0, 0, 0};
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -153,6 +158,9 @@ void free_device(DevCtx& d) {
   if (d.bits) (void)hipFree(d.bits);
   if (d.recs) (void)hipFree(d.recs);
   if (d.pool) (void)hipFree(d.pool);
+  if (d.txt) (void)hipFree(d.txt);
+  for (auto p : d.stage)
+    if (p) (void)hipFree(p);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d = DevCtx();
@@ -193,6 +201,63 @@ int self_check(DevCtx& d) {
       g_last_hip = "self-check: generated valid signatures did not verify";
       return HKV_E_INTERNAL;
     }
+  return HKV_OK;
+}
+
+// ---- signature hashes / standard inputs ------------------------------------
+
+int grow(void** p, size_t* cap, size_t bytes, const char* what) {
+  if (*cap >= bytes && *p) return HKV_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HKV_TRY(hipMalloc(p, bytes ? bytes : 16), what);
+  *cap = bytes;
+  return HKV_OK;
+}
+
+bool txs_ok(const hkv_txs* t) {
+  return t && (t->n_tx == 0 || (t->bytes && t->offsets)) && (t->scripts || t->scripts_len == 0) &&
+         t->n_tx < 0xFFFFFF00u;
+}
+
+int enqueue_tx_index(DevCtx& d, const hkv_txs* dt, hipStream_t st) {
+  int rc = grow(reinterpret_cast<void**>(&d.txt), &d.txt_cap, (size_t)dt->n_tx * hkv::TXT_WORDS * 4, "hipMalloc(txt)");
+  if (rc) return rc;
+  HKV_TRY(hkv::launch_tx_index(dt->bytes, dt->offsets, dt->n_tx, 1u, d.txt, st), "tx index launch");
+  return HKV_OK;
+}
+
+int enqueue_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                       void* recs, hipStream_t st) {
+  int rc = enqueue_tx_index(d, dt, st);
+  if (rc) return rc;
+  HKV_TRY(hkv::launch_std_inputs(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
+                                 static_cast<uint8_t*>(recs), st),
+          "std input launch");
+  return HKV_OK;
+}
+
+// copy a host tx batch (+ jobs) into the device's staging buffers
+int stage_txs(DevCtx& d, const hkv_txs* h, const void* jobs, size_t job_bytes, hkv_txs* dt, void** djobs) {
+  const size_t nbytes = h->n_tx ? h->offsets[h->n_tx] : 0;
+  const size_t noff = ((size_t)h->n_tx + 1) * 4;
+  int rc = grow(&d.stage[0], &d.stage_cap[0], nbytes, "hipMalloc(tx bytes)");
+  if (!rc) rc = grow(&d.stage[1], &d.stage_cap[1], noff, "hipMalloc(tx offsets)");
+  if (!rc) rc = grow(&d.stage[2], &d.stage_cap[2], h->scripts_len, "hipMalloc(scripts)");
+  if (!rc) rc = grow(&d.stage[3], &d.stage_cap[3], job_bytes, "hipMalloc(jobs)");
+  if (rc) return rc;
+  if (nbytes) HKV_TRY(hipMemcpyAsync(d.stage[0], h->bytes, nbytes, hipMemcpyHostToDevice, d.stream), "H2D txs");
+  if (h->n_tx) HKV_TRY(hipMemcpyAsync(d.stage[1], h->offsets, noff, hipMemcpyHostToDevice, d.stream), "H2D offsets");
+  if (h->scripts_len)
+    HKV_TRY(hipMemcpyAsync(d.stage[2], h->scripts, h->scripts_len, hipMemcpyHostToDevice, d.stream), "H2D scripts");
+  if (job_bytes) HKV_TRY(hipMemcpyAsync(d.stage[3], jobs, job_bytes, hipMemcpyHostToDevice, d.stream), "H2D jobs");
+  dt->bytes = static_cast<const uint8_t*>(d.stage[0]);
+  dt->offsets = static_cast<const uint32_t*>(d.stage[1]);
+  dt->n_tx = h->n_tx;
+  dt->scripts = static_cast<const uint8_t*>(d.stage[2]);
+  dt->scripts_len = h->scripts_len;
+  *djobs = d.stage[3];
   return HKV_OK;
 }
 
@@ -420,6 +485,132 @@ int hkv_profile_read(hkv_ctx* ctx, int dev, double* prologue_ms, double* ecmult_
   *ecmult_ms = m;
   *launches = d.ev.size() / 3;
   clear_events(d);
+  return HKV_OK;
+}
+
+int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_sighash_job* d_jobs, size_t n,
+                       int32_t forkid, uint8_t* d_out, size_t out_stride, uint8_t* d_status, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || out_stride < 32 || out_stride % 4 ||
+      out_stride > 0xFFFFFFFFu || n > 0xFFFFFF00ull)
+    return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!d_jobs || !d_out) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  int rc = enqueue_tx_index(d, d_txs, st);
+  if (rc) return rc;
+  HKV_TRY(hkv::launch_sighash(d_txs->bytes, d_txs->n_tx, d.txt, d_txs->scripts, d_txs->scripts_len, d_jobs,
+                              (uint32_t)n, forkid, d_out, (uint32_t)out_stride, d_status, st),
+          "sighash launch");
+  return HKV_OK;
+}
+
+int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, size_t n, int32_t forkid,
+                uint8_t* out32, uint8_t* status) {
+  if (!ctx || ctx->devs.empty() || !txs_ok(txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!jobs || !out32) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[0];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hkv_txs dt;
+  void* djobs = nullptr;
+  int rc = stage_txs(d, txs, jobs, n * sizeof(hkv_sighash_job), &dt, &djobs);
+  if (!rc) rc = grow(&d.stage[4], &d.stage_cap[4], n * 33, "hipMalloc(sighash out)");
+  if (!rc) rc = enqueue_tx_index(d, &dt, d.stream);
+  if (rc) return rc;
+  uint8_t* dout = static_cast<uint8_t*>(d.stage[4]);
+  HKV_TRY(hkv::launch_sighash(dt.bytes, dt.n_tx, d.txt, dt.scripts, dt.scripts_len,
+                              static_cast<const hkv_sighash_job*>(djobs), (uint32_t)n, forkid, dout, 32, dout + n * 32,
+                              d.stream),
+          "sighash launch");
+  HKV_TRY(hipMemcpyAsync(out32, dout, n * 32, hipMemcpyDeviceToHost, d.stream), "D2H sighash");
+  if (status) HKV_TRY(hipMemcpyAsync(status, dout + n * 32, n, hipMemcpyDeviceToHost, d.stream), "D2H status");
+  HKV_TRY(hipStreamSynchronize(d.stream), "sighash sync");
+  return HKV_OK;
+}
+
+int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
+                          int32_t forkid, void* d_records, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!d_jobs || !d_records) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  return enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
+}
+
+int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
+                                 int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!d_jobs || !d_records || !d_bits) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  int rc = enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
+  if (!rc) rc = enqueue_verify(d, d_records, n, HKV_MODE_HASKOIN, st);
+  if (rc) return rc;
+  HKV_TRY(hipMemcpyAsync(d_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
+  return HKV_OK;
+}
+
+int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                          uint32_t* verdict_bits) {
+  if (!ctx || ctx->devs.empty() || !txs_ok(txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!jobs || !verdict_bits) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[0];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hkv_txs dt;
+  void* djobs = nullptr;
+  int rc = stage_txs(d, txs, jobs, n * sizeof(hkv_input_job), &dt, &djobs);
+  if (!rc && d.recs_cap < n) {
+    if (d.recs) (void)hipFree(d.recs);
+    d.recs = nullptr;
+    d.recs_cap = 0;
+    HKV_TRY(hipMalloc(&d.recs, n * hkv::REC_SIZE), "hipMalloc(records)");
+    d.recs_cap = n;
+  }
+  if (!rc) rc = enqueue_std_inputs(d, &dt, static_cast<const hkv_input_job*>(djobs), n, forkid, d.recs, d.stream);
+  if (!rc) rc = enqueue_verify(d, d.recs, n, HKV_MODE_HASKOIN, d.stream);
+  if (rc) return rc;
+  HKV_TRY(hipMemcpyAsync(verdict_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
+  HKV_TRY(hipStreamSynchronize(d.stream), "std inputs sync");
+  return HKV_OK;
+}
+
+int hkv_gen_keys_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint8_t* d_priv, uint8_t* d_pub,
+                        uint8_t* d_h160, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!d_priv || !d_pub || !d_h160) return HKV_E_ARG;
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  HKV_TRY(hkv::launch_gen_keys(seed, (uint32_t)n, d_priv, d_pub, d_h160, st), "gen keys launch");
+  return HKV_OK;
+}
+
+int hkv_gen_sign_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, const uint8_t* d_priv,
+                        const uint32_t* d_key_idx, const uint8_t* d_msg, size_t msg_stride, uint8_t* d_sig,
+                        void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || n > 0xFFFFFF00ull || msg_stride < 32 ||
+      msg_stride > 0xFFFFFFFFu)
+    return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!d_priv || !d_msg || !d_sig) return HKV_E_ARG;
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  HKV_TRY(hkv::launch_gen_sign(seed, (uint32_t)n, d_priv, d_key_idx, d_msg, (uint32_t)msg_stride, d_sig, st),
+          "gen sign launch");
   return HKV_OK;
 }
 

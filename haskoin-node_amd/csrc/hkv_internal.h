@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/hkv.h"
+
 #define HKV_MODE_LIBSECP 0u
 #define HKV_MODE_HASKOIN 1u
 
@@ -34,4 +36,16 @@ hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, u
 hipError_t launch_debug(uint32_t op, uint32_t n, const uint32_t* a, const uint32_t* b, uint32_t* out,
                         hipStream_t st);
 hipError_t ecmult_max_blocks_per_cu(int* out);
+hipError_t launch_gen_keys(uint64_t seed, uint32_t n, uint8_t* priv, uint8_t* pub, uint8_t* h160, hipStream_t st);
+hipError_t launch_gen_sign(uint64_t seed, uint32_t n, const uint8_t* priv, const uint32_t* key_idx,
+                           const uint8_t* msg, uint32_t msg_stride, uint8_t* sig, hipStream_t st);
+// hkv_sighash.hip
+hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t want_bip143,
+                           uint32_t* txt, hipStream_t st);
+hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                          uint32_t scripts_len, const hkv_sighash_job* jobs, uint32_t n, int32_t forkid, uint8_t* out,
+                          uint32_t stride, uint8_t* status, hipStream_t st);
+hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                             uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
+                             uint8_t* recs, hipStream_t st);
 }  // namespace hkv

@@ -20,6 +20,7 @@
 // secp256k1_ecdsa_verify, and haskoin-core verifyHashSig (normalize first)
 // [dep; pinned /root/reference/stack.yaml:8-10; SURVEY.md §8(a) a1, a3-a6].
 #include "hkv_group.h"
+#include "hkv_hash.h"
 #include "hkv_layout.h"
 #include "hkv_internal.h"
 
@@ -640,6 +641,77 @@ __global__ void __launch_bounds__(WG) hkv_gen_records_kernel(uint64_t seed, uint
   for (int k = 162; k < REC_SIZE; ++k) o[k] = 0;
 }
 
+// Block-mix generator hooks (bench.py configs[2], tests): random keys with
+// their compressed pubkey and HASH160, and ECDSA signatures of given msg32s.
+__global__ void __launch_bounds__(WG) hkv_gen_keys_kernel(uint64_t seed, uint32_t n, uint8_t* __restrict__ priv,
+                                                          uint8_t* __restrict__ pub, uint8_t* __restrict__ h160) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st = seed * 0x9FB21C651E98DF25ull + (uint64_t)i * 0x9E3779B97F4A7C15ull + 0x2545F4914F6CDD1Dull;
+  sc d, zero;
+  rand_scalar(d, st);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) zero.v[k] = 0;
+  ge g, q;
+  ge_set_g(g);
+  ecmult_simple(q, d, zero, g);
+  put_be256(priv + (size_t)i * 32, d.v);
+  uint8_t* pk = pub + (size_t)i * 33;
+  pk[0] = (uint8_t)(2u | (q.y.v[0] & 1u));
+  put_be256(pk + 1, q.x.v);
+  // HASH160 = RIPEMD160(SHA256(pk)): one SHA-256 block of 33 bytes
+  uint32_t w[16], h[8], rip[5];
+  w[0] = ((uint32_t)pk[0] << 24) | (q.x.v[7] >> 8);
+#pragma unroll
+  for (int k = 1; k < 8; ++k) w[k] = (q.x.v[8 - k] << 24) | (q.x.v[7 - k] >> 8);
+  w[8] = (q.x.v[0] << 24) | 0x800000u;
+#pragma unroll
+  for (int k = 9; k < 15; ++k) w[k] = 0;
+  w[15] = 33 * 8;
+  sha256_init(h);
+  sha256_compress(h, w);
+  ripemd160_of_digest(rip, h);
+  uint8_t* o = h160 + (size_t)i * 20;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) o[k] = (uint8_t)(rip[k >> 2] >> (8 * (k & 3)));
+}
+
+__global__ void __launch_bounds__(WG) hkv_gen_sign_kernel(uint64_t seed, uint32_t n, const uint8_t* __restrict__ priv,
+                                                          const uint32_t* __restrict__ key_idx,
+                                                          const uint8_t* __restrict__ msg, uint32_t msg_stride,
+                                                          uint8_t* __restrict__ sig) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st = seed * 0xC2B2AE3D27D4EB4Full + (uint64_t)i * 0x9E3779B97F4A7C15ull + 0x165667B19E3779F9ull;
+  const uint32_t kidx = key_idx ? key_idx[i] : i;
+  sc d, m, k, zero, r, s, t, ki;
+  const uint8_t* dp = priv + (size_t)kidx * 32;
+  const uint8_t* mp = msg + (size_t)i * msg_stride;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    d.v[7 - q] = ((uint32_t)dp[4 * q] << 24) | ((uint32_t)dp[4 * q + 1] << 16) | ((uint32_t)dp[4 * q + 2] << 8) |
+                 dp[4 * q + 3];
+    m.v[7 - q] = ((uint32_t)mp[4 * q] << 24) | ((uint32_t)mp[4 * q + 1] << 16) | ((uint32_t)mp[4 * q + 2] << 8) |
+                 mp[4 * q + 3];
+    zero.v[q] = 0;
+  }
+  sc_cond_sub_n(m.v);
+  rand_scalar(k, st);
+  ge g, R;
+  ge_set_g(g);
+  ecmult_simple(R, k, zero, g);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) r.v[q] = R.x.v[q];
+  sc_cond_sub_n(r.v);
+  sc_mul(t, r, d);
+  sc_add(t, t, m);
+  sc_inv(ki, k);
+  sc_mul(s, ki, t);
+  if (sc_is_high(s)) sc_neg(s, s);
+  put_be256(sig + (size_t)i * 64, r.v);
+  put_be256(sig + (size_t)i * 64 + 32, s.v);
+}
+
 // ---------------------------------------------------------------------------
 // debug / known-answer kernel for the tests (field, scalar, GLV ops)
 // ---------------------------------------------------------------------------
@@ -739,6 +811,16 @@ hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, u
 hipError_t launch_debug(uint32_t op, uint32_t n, const uint32_t* a, const uint32_t* b, uint32_t* out,
                         hipStream_t st) {
   hipLaunchKernelGGL(hkv_debug_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, op, n, a, b, out);
+  return hipGetLastError();
+}
+hipError_t launch_gen_keys(uint64_t seed, uint32_t n, uint8_t* priv, uint8_t* pub, uint8_t* h160, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_gen_keys_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, seed, n, priv, pub, h160);
+  return hipGetLastError();
+}
+hipError_t launch_gen_sign(uint64_t seed, uint32_t n, const uint8_t* priv, const uint32_t* key_idx,
+                           const uint8_t* msg, uint32_t msg_stride, uint8_t* sig, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_gen_sign_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, seed, n, priv, key_idx, msg,
+                     msg_stride, sig);
   return hipGetLastError();
 }
 hipError_t ecmult_max_blocks_per_cu(int* out) {

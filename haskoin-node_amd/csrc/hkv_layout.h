@@ -56,6 +56,27 @@ constexpr int QTAB_QUADS = QTAB_ENTRIES * QTAB_QUADS_PER_ENTRY;
 
 constexpr int WG = 256;                // threads per workgroup (4 waves)
 
+// Per-transaction index (hkv_sighash.hip, tx index kernel), AoS rows of
+// TXT_WORDS words so a job's gather of its tx row is one 128-byte line.
+// Offsets are absolute byte offsets into the batch's tx buffer. The three
+// BIP143 hashes are stored in digest byte order (word k = bytes 4k..4k+3,
+// little-endian), i.e. exactly as they appear in a preimage.
+enum : int {
+  TXT_FLAGS = 0,        // bit0 parsed ok, bit1 witness serialisation
+  TXT_INS = 1,          // first input
+  TXT_NIN = 2,
+  TXT_NOUT = 3,
+  TXT_OUTS_FIRST = 4,   // first output (after the count varint)
+  TXT_OUTS_END = 5,     // end of outputs = start of the witness section
+  TXT_LOCK = 6,         // locktime
+  TXT_START = 7,        // first byte of the tx (version)
+  TXT_HP = 8,           // hashPrevouts
+  TXT_HS = 16,          // hashSequence
+  TXT_HO = 24,          // hashOutputs
+  TXT_WORDS = 32,
+};
+constexpr uint32_t TXF_OK = 1u, TXF_WITNESS = 2u;
+
 // minimum waves per SIMD the ecmult kernel's register allocation targets
 #ifndef HKV_ECMULT_WAVES
 #define HKV_ECMULT_WAVES 4

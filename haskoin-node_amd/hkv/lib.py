@@ -11,6 +11,11 @@ HKV_RECORD_SIZE = 168
 HKV_LIBSECP = 0
 HKV_HASKOIN = 1
 
+HKV_SIGHASH_LEGACY = 0
+HKV_SIGHASH_FORKID = 1
+HKV_NO_FORKID = -1
+HKV_SH_OK, HKV_SH_BAD_TX, HKV_SH_BAD_INPUT, HKV_SH_BAD_REF = 0, 1, 2, 3
+
 HKV_OK = 0
 _ERRS = {-1: "HKV_E_ARG", -2: "HKV_E_NODEV", -3: "HKV_E_OOM", -4: "HKV_E_HIP", -5: "HKV_E_INTERNAL"}
 
@@ -33,6 +38,24 @@ class HkvError(RuntimeError):
         self.rc = rc
 
 
+class HkvTxs(ctypes.Structure):
+    """struct hkv_txs (include/hkv.h)."""
+    _fields_ = [("bytes", c_void_p), ("offsets", c_void_p), ("n_tx", c_uint32), ("scripts", c_void_p),
+                ("scripts_len", c_uint32)]
+
+
+class HkvSighashJob(ctypes.Structure):
+    _fields_ = [("tx", c_uint32), ("input", c_uint32), ("script_off", c_uint32), ("script_len", c_uint32),
+                ("value", c_uint64), ("sighash", c_uint32), ("kind", c_uint32)]
+
+
+class HkvInputJob(ctypes.Structure):
+    _fields_ = [("tx", c_uint32), ("input", c_uint32), ("script_off", c_uint32), ("script_len", c_uint32),
+                ("value", c_uint64)]
+
+
+assert ctypes.sizeof(HkvSighashJob) == 32 and ctypes.sizeof(HkvInputJob) == 24
+
 # name -> (restype, argtypes)
 EXPORTS = {
     "hkv_open": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
@@ -48,6 +71,18 @@ EXPORTS = {
     "hkv_verify_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint32, c_void_p, c_void_p]),
     "hkv_gen_records_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_uint32, c_uint32, c_void_p,
                                        c_void_p]),
+    "hkv_sighash": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p, c_void_p]),
+    "hkv_sighash_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p,
+                                   c_size_t, c_void_p, c_void_p]),
+    "hkv_std_inputs_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
+                                      c_void_p, c_void_p]),
+    "hkv_verify_std_inputs_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
+                                             c_void_p, c_void_p, c_void_p]),
+    "hkv_verify_std_inputs": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
+                                      POINTER(c_uint32)]),
+    "hkv_gen_keys_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hkv_gen_sign_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_void_p, c_void_p, c_void_p, c_size_t,
+                                    c_void_p, c_void_p]),
     "hkv_debug_op": (c_int, [c_void_p, c_int, c_uint32, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hkv_profile_enable": (c_int, [c_void_p, c_int]),
     "hkv_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),

@@ -92,6 +92,40 @@ class Verifier:
                                              ctypes.c_void_p(stream_ptr or None))
         check(rc, "hkv_gen_records_device", self.lib)
 
+    # -- signature hashes / standard inputs on device (hkv_*_device) ---------
+    def sighash_device(self, dev: int, d_txs, d_jobs: int, n: int, forkid: int, d_out: int, out_stride: int,
+                       d_status: int = 0, stream_ptr: int = 0) -> None:
+        rc = self.lib.hkv_sighash_device(self.ctx, dev, ctypes.byref(d_txs), ctypes.c_void_p(d_jobs), n, forkid,
+                                         ctypes.c_void_p(d_out), out_stride, ctypes.c_void_p(d_status or None),
+                                         ctypes.c_void_p(stream_ptr or None))
+        check(rc, "hkv_sighash_device", self.lib)
+
+    def std_inputs_device(self, dev: int, d_txs, d_jobs: int, n: int, forkid: int, d_records: int,
+                          stream_ptr: int = 0) -> None:
+        rc = self.lib.hkv_std_inputs_device(self.ctx, dev, ctypes.byref(d_txs), ctypes.c_void_p(d_jobs), n, forkid,
+                                            ctypes.c_void_p(d_records), ctypes.c_void_p(stream_ptr or None))
+        check(rc, "hkv_std_inputs_device", self.lib)
+
+    def verify_std_inputs_device(self, dev: int, d_txs, d_jobs: int, n: int, forkid: int, d_records: int,
+                                 d_bits: int, stream_ptr: int = 0) -> None:
+        rc = self.lib.hkv_verify_std_inputs_device(self.ctx, dev, ctypes.byref(d_txs), ctypes.c_void_p(d_jobs), n,
+                                                   forkid, ctypes.c_void_p(d_records), ctypes.c_void_p(d_bits),
+                                                   ctypes.c_void_p(stream_ptr or None))
+        check(rc, "hkv_verify_std_inputs_device", self.lib)
+
+    def gen_keys_device(self, dev: int, seed: int, n: int, d_priv: int, d_pub: int, d_h160: int,
+                        stream_ptr: int = 0) -> None:
+        rc = self.lib.hkv_gen_keys_device(self.ctx, dev, seed, n, ctypes.c_void_p(d_priv), ctypes.c_void_p(d_pub),
+                                          ctypes.c_void_p(d_h160), ctypes.c_void_p(stream_ptr or None))
+        check(rc, "hkv_gen_keys_device", self.lib)
+
+    def gen_sign_device(self, dev: int, seed: int, n: int, d_priv: int, d_key_idx: int, d_msg: int, msg_stride: int,
+                        d_sig: int, stream_ptr: int = 0) -> None:
+        rc = self.lib.hkv_gen_sign_device(self.ctx, dev, seed, n, ctypes.c_void_p(d_priv),
+                                          ctypes.c_void_p(d_key_idx or None), ctypes.c_void_p(d_msg), msg_stride,
+                                          ctypes.c_void_p(d_sig), ctypes.c_void_p(stream_ptr or None))
+        check(rc, "hkv_gen_sign_device", self.lib)
+
     def debug_op(self, dev: int, op: int, n: int, d_a: int, d_b: int, d_out: int, stream_ptr: int = 0) -> None:
         rc = self.lib.hkv_debug_op(self.ctx, dev, op, n, ctypes.c_void_p(d_a), ctypes.c_void_p(d_b),
                                    ctypes.c_void_p(d_out), ctypes.c_void_p(stream_ptr or None))

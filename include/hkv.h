@@ -20,6 +20,17 @@
  *   hkv_open / hkv_close
  *       replaces secp256k1-haskell `createContext`/`withContext` (one
  *       shared read-only context per process).
+ *   hkv_sighash / hkv_sighash_device
+ *       replaces N calls of haskoin-core
+ *       `txSigHash :: Network -> Tx -> Script -> Word64 -> Int -> SigHash -> Hash256`
+ *       and `txSigHashForkId` (Haskoin.Script.SigHash) — the producer of
+ *       every msg32 verifyHashSig checks.
+ *   hkv_verify_std_inputs / hkv_verify_std_inputs_device
+ *       replaces N calls of haskoin-core
+ *       `verifyStdInput :: Network -> Ctx -> Tx -> Int -> ScriptOutput -> Word64 -> Bool`
+ *       (Haskoin.Transaction.Builder) for P2PK / P2PKH / P2WPKH prevouts:
+ *       decodeTxSig (strict DER, low S, hashtype), HASH160 check, sighash and
+ *       verifyHashSig, all on device.
  *
  * Conventions: no C++ exceptions cross this boundary; every function that
  * can fail returns 0 (HKV_OK) or a negative hkv_err. A verdict is never an
@@ -102,6 +113,93 @@ int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, ui
  * share of uncompressed keys, all signatures low-S. Enqueued on hip_stream. */
 int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
                            uint32_t uncompressed_permille, void* d_records, void* hip_stream);
+
+/* ------------------------------------------------------------------------
+ * Signature hashes and standard inputs on device (SURVEY.md §8(a) a7-a9,
+ * §8(f) row 2).
+ *
+ * A tx batch is a buffer of serialised transactions (wire form, BIP144
+ * witness form allowed) with n_tx + 1 byte offsets (tx t occupies
+ * bytes[offsets[t], offsets[t+1])), plus a pool of scripts the jobs refer to
+ * by (offset, length). In the *_device entry points every pointer of the
+ * hkv_txs and the job / output arrays live in HBM of device `dev`.
+ * ------------------------------------------------------------------------ */
+typedef struct hkv_txs {
+  const uint8_t* bytes;
+  const uint32_t* offsets; /* n_tx + 1 entries, non-decreasing, < 2^32 */
+  uint32_t n_tx;
+  const uint8_t* scripts;
+  uint32_t scripts_len;
+} hkv_txs;
+
+#define HKV_SIGHASH_LEGACY 0u /* haskoin-core txSigHash                  */
+#define HKV_SIGHASH_FORKID 1u /* haskoin-core txSigHashForkId (BIP143)   */
+#define HKV_NO_FORKID (-1)    /* network without a fork id (BTC)         */
+
+/* One call of txSigHash / txSigHashForkId:
+ *   txSigHash net tx scriptCode value input sighash
+ * scriptCode = scripts[script_off, script_off + script_len). 32 bytes. */
+typedef struct hkv_sighash_job {
+  uint32_t tx;
+  uint32_t input;
+  uint32_t script_off;
+  uint32_t script_len;
+  uint64_t value;   /* prevout amount (BIP143 form) */
+  uint32_t sighash; /* SigHash word */
+  uint32_t kind;    /* HKV_SIGHASH_LEGACY / HKV_SIGHASH_FORKID */
+} hkv_sighash_job;
+
+/* per-job status (hkv_sighash*): the hash of a failed job is all zero */
+#define HKV_SH_OK 0u
+#define HKV_SH_BAD_TX 1u    /* the tx does not parse within its bounds   */
+#define HKV_SH_BAD_INPUT 2u /* input index >= number of inputs           */
+#define HKV_SH_BAD_REF 3u   /* tx index or script range out of the batch */
+
+/* One standard input for verifyStdInput: input `input` of tx `tx` spends a
+ * prevout with scriptPubKey = scripts[script_off, +script_len) and amount
+ * `value`. Templates: P2PK (21 <33> ac / 41 <65> ac), P2PKH, P2WPKH; any other
+ * prevout script verifies false. 24 bytes. */
+typedef struct hkv_input_job {
+  uint32_t tx;
+  uint32_t input;
+  uint32_t script_off;
+  uint32_t script_len;
+  uint64_t value;
+} hkv_input_job;
+
+/* Batch txSigHash / txSigHashForkId (forkid: HKV_NO_FORKID or the network's
+ * fork id, e.g. 0 for BCH). out32: n * 32 bytes; status: n bytes or NULL.
+ * Host memory; runs on the context's first device. Blocking. */
+int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, size_t n, int32_t forkid,
+                uint8_t* out32, uint8_t* status);
+/* Device form: hash j goes to d_out + j * out_stride (out_stride % 4 == 0;
+ * 168 writes the msg32 field of verify records in place). Enqueued on
+ * hip_stream, not synchronised. */
+int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_sighash_job* d_jobs, size_t n,
+                       int32_t forkid, uint8_t* d_out, size_t out_stride, uint8_t* d_status, void* hip_stream);
+/* The non-ECDSA half of verifyStdInput on device: one 168-byte verify record
+ * per input (all-zero when the template / DER / HASH160 checks fail). */
+int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
+                          int32_t forkid, void* d_records, void* hip_stream);
+/* Full batch verifyStdInput: extraction + ECDSA (HKV_HASKOIN semantics).
+ * d_records: scratch of n * 168 bytes; verdict bit i in d_bits
+ * (>= ceil(n/64)*2 words). Enqueued on hip_stream, not synchronised. */
+int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
+                                 int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream);
+/* Host-memory form of the above; writes ceil(n/32) verdict words. Blocking. */
+int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                          uint32_t* verdict_bits);
+
+/* Synthetic-data hooks (block-mix generator, off the verify path):
+ * n random private keys -> d_priv (n*32, big-endian), compressed public keys
+ * d_pub (n*33) and their HASH160 d_h160 (n*20);
+ * ECDSA signatures (r||s big-endian, low S, random nonces) of msg j
+ * (d_msg + j*msg_stride) with key d_key_idx[j] -> d_sig (n*64). */
+int hkv_gen_keys_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint8_t* d_priv, uint8_t* d_pub,
+                        uint8_t* d_h160, void* hip_stream);
+int hkv_gen_sign_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, const uint8_t* d_priv,
+                        const uint32_t* d_key_idx, const uint8_t* d_msg, size_t msg_stride, uint8_t* d_sig,
+                        void* hip_stream);
 
 /* Known-answer hook for the tests: applies op (see hkv_internal.h) to n
  * pairs of 8-limb little-endian operands in device memory; 16 words out. */

@@ -1,0 +1,256 @@
+"""GPU parity tests (MI355X) for the on-device signature hashes and standard
+inputs: the HIP kernels through the C
+ABI against oracle/sighash_oracle.py — byte-exact hashes, byte-exact verify
+records and bit-exact verdicts, including malformed and adversarial inputs."""
+import ctypes
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import secp256k1_oracle as o
+import sighash_oracle as sh
+import txgen
+from conftest import GOLDEN, oracle_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need the MI355X"
+    return t
+
+
+@pytest.fixture(scope="module")
+def ver(torch):
+    import hkv
+    v = hkv.Verifier(hkv.VerifierConfig(device_ids=[0], flags=1))
+    yield v
+    v.close()
+
+
+def oracle_sighash(raw_txs, jobs, forkid):
+    out = []
+    for (t, i, code, value, shw, kind) in jobs:
+        tx = sh.tx_parse(raw_txs[t])
+        if kind == sh.KIND_LEGACY and not (forkid is not None and shw & 0x40) and (shw & 0x1F) == 3 \
+                and i >= len(tx.outputs):
+            out.append(sh.ONE)
+        else:
+            out.append(sh.sighash_job(tx, kind, code, value, i, shw, forkid))
+    return out
+
+
+def random_jobs(rng, raw_txs, n_jobs):
+    jobs = []
+    for _ in range(n_jobs):
+        t = rng.randrange(len(raw_txs))
+        nin = len(sh.tx_parse(raw_txs[t]).inputs)
+        jobs.append((t, rng.randrange(nin), txgen.rand_code(rng), rng.randrange(2**64), txgen.rand_sighash(rng),
+                     rng.randrange(2)))
+    return jobs
+
+
+@pytest.mark.parametrize("forkid", [None, 0, 7])
+def test_sighash_random_vs_oracle(ver, forkid):
+    import hkv
+    rng = random.Random(100 + (forkid or 0))
+    txs = []
+    for k in range(300):
+        nin, nout = rng.choice([1, 1, 2, 3, 5, 17]), rng.choice([0, 1, 2, 3, 9])
+        txs.append(sh.tx_serialize(txgen.rand_tx(rng, nin, nout, segwit=(k % 3 == 0))))
+    txs.append(sh.tx_serialize(txgen.rand_tx(rng, 3, 3, big_scripts=True)))  # 0xFD / 0xFE varints
+    jobs = random_jobs(rng, txs, 2500)
+    jobs += [(len(txs) - 1, i, txgen.rand_code(rng), 5, s, k) for i in range(3) for s in (1, 2, 3, 0x83)
+             for k in (0, 1)]
+    got, status = hkv.tx_sig_hash_batch(ver, txs, jobs, forkid)
+    exp = oracle_sighash(txs, jobs, forkid)
+    assert all(s == 0 for s in status)
+    bad = [k for k in range(len(jobs)) if got[k] != exp[k]]
+    assert not bad, [(jobs[k][3:], got[k].hex(), exp[k].hex()) for k in bad[:5]]
+
+
+def test_sighash_bip143_example(ver):
+    import hkv
+    b = json.load(open(os.path.join(GOLDEN, "bip143_p2wpkh.json")))
+    raw = bytes.fromhex(b["unsigned_tx"])
+    i0, i1 = b["inputs"]
+    h20 = bytes.fromhex(i1["script_pubkey"])[2:]
+    got, status = hkv.tx_sig_hash_batch(ver, [raw], [
+        (0, 1, sh.p2pkh_script(h20), i1["value"], 1, hkv.HKV_SIGHASH_FORKID),
+        (0, 0, bytes.fromhex(i0["script_pubkey"]), i0["value"], 1, hkv.HKV_SIGHASH_LEGACY)])
+    assert status == [0, 0]
+    assert got[0].hex() == b["input1_sighash_all"]["sigHash"]
+    tx = sh.tx_parse(raw)
+    assert got[1] == sh.sighash_legacy(tx, bytes.fromhex(i0["script_pubkey"]), 0, 0, 1)
+
+
+def test_sighash_noncanonical_varints_and_errors(ver):
+    import hkv
+    rng = random.Random(7)
+    tx = txgen.rand_tx(rng, 2, 2)
+    tx.outputs[1].script = b"\x76" * 25
+    raw = sh.tx_serialize(tx)
+    # re-encode output 1's script length 0x19 as FD 19 00 (non-canonical)
+    k = raw.rfind(bytes([25]) + b"\x76" * 25)
+    nc = raw[:k] + b"\xfd\x19\x00" + raw[k + 1:]
+    assert sh.tx_parse(nc).outputs[1].script == b"\x76" * 25
+    code = sh.p2pkh_script(b"\x22" * 20)
+    jobs = [(0, 0, code, 9, s, kind) for s in (1, 3, 0x81) for kind in (0, 1)]
+    got, st = hkv.tx_sig_hash_batch(ver, [nc], jobs)
+    assert st == [0] * len(jobs)
+    assert got == oracle_sighash([nc], jobs, None)
+    assert got == oracle_sighash([raw], jobs, None)  # haskoin hashes the re-serialised tx
+    # errors: truncated tx, input out of range, tx index out of range
+    trunc = raw[:-5]
+    got, st = hkv.tx_sig_hash_batch(ver, [trunc, raw], [(0, 0, code, 0, 1, 0), (1, 2, code, 0, 1, 0),
+                                                        (1, 1, code, 0, 1, 1)])
+    assert st == [hkv.lib.HKV_SH_BAD_TX, hkv.lib.HKV_SH_BAD_INPUT, 0]
+    assert got[0] == b"\0" * 32 and got[1] == b"\0" * 32
+    # the ABI rejects a job that points past the batch only per job (status), not the call
+    from hkv.sighash import SIGHASH_JOB_DTYPE, TxBatch
+    tb = TxBatch([raw])
+    arr = np.zeros(2, dtype=SIGHASH_JOB_DTYPE)
+    arr[0] = (5, 0, 0, 0, 0, 1, 0)
+    arr[1] = (0, 0, 0, 10_000, 0, 1, 0)
+    st_, pool = tb.struct()
+    out = np.zeros((2, 32), dtype=np.uint8)
+    status = np.zeros(2, dtype=np.uint8)
+    assert ver.lib.hkv_sighash(ver.ctx, ctypes.byref(st_), arr.ctypes.data, 2, -1, out.ctypes.data,
+                               status.ctypes.data) == 0
+    assert list(status) == [3, 3]
+
+
+# --- standard inputs -----------------------------------------------------------
+
+def upload(torch, arr: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy()).cuda()
+
+
+def device_std_records(torch, ver, raw_txs, inputs, forkid):
+    """Run hkv_std_inputs_device and return the 168-byte records."""
+    import hkv
+    from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
+    tb = TxBatch(raw_txs)
+    arr = np.zeros(len(inputs), dtype=INPUT_JOB_DTYPE)
+    for k, (t, i, spk, value) in enumerate(inputs):
+        off, ln = tb.script(spk)
+        arr[k] = (t, i, off, ln, value)
+    _, pool = tb.struct()
+    d_bytes, d_off, d_pool, d_jobs = upload(torch, tb.bytes), upload(torch, tb.offsets), upload(torch, pool), \
+        upload(torch, arr)
+    dt = hkv.HkvTxs(d_bytes.data_ptr(), d_off.data_ptr(), len(raw_txs), d_pool.data_ptr(), tb._len)
+    recs = torch.zeros(len(inputs) * 168, dtype=torch.uint8, device="cuda")
+    ver.std_inputs_device(0, dt, d_jobs.data_ptr(), len(inputs), -1 if forkid is None else forkid, recs.data_ptr())
+    torch.cuda.synchronize()
+    return recs.cpu().numpy().tobytes()
+
+
+def mutate_block(rng, txs, jobs, forkid):
+    """Adversarial copies of signed inputs (one mutation each)."""
+    out_txs, out_jobs, kinds = [], [], []
+    for m in range(14):
+        for (t, i, prev, val) in rng.sample(jobs, 6):
+            tx = sh.tx_parse(sh.tx_serialize(txs[t]))
+            seg = len(prev) == 22
+            sig = tx.witness[i][0] if seg else sh._push_items(tx.inputs[i].script)[0]
+            pub = tx.witness[i][1] if seg else (sh._push_items(tx.inputs[i].script) + [b""])[1]
+            r, s = sh.sig_parse_der(sig[:-1])
+            if m == 0:
+                sig = sig[:5] + bytes([sig[5] ^ 1]) + sig[6:]           # r byte flipped: ECDSA fails
+            elif m == 1:
+                sig = sh.der_encode(r, o.N - s) + sig[-1:]              # high S: strict decode fails
+            elif m == 2:
+                sig = sig[:-1] + b"\x04"                                 # unknown hashtype
+            elif m == 3:
+                sig = sig[:-1] + b"\x41"                                 # FORKID byte
+            elif m == 4:
+                sig = sig[:1] + b"\x81" + sig[1:2] + sig[2:]            # long-form length < 128
+            elif m == 5:
+                sig = sig + b"\x00"                                      # trailing byte (after hashtype)
+            elif m == 6:
+                pub = txgen.Key(rng.randrange(1, o.N)).pub               # HASH160 mismatch
+            elif m == 7:
+                prev = prev[:-1] + b"\x00"                               # not a template
+            elif m == 8:
+                val += 1                                                 # wrong amount (BIP143 only)
+            elif m == 9:
+                sig = sh.der_encode(r, s) + b"\x03"                      # SIGHASH_SINGLE: other msg
+            elif m == 10:
+                sig = sig[:-1] + b"\x81"                                 # ANYONECANPAY|ALL: other msg
+            elif m == 11:
+                sig = b"\x30\x06\x02\x01\x00\x02\x01\x01\x01"           # r = 0
+            elif m == 12:
+                sig = sh.der_encode(o.N + 5, s) + sig[-1:]               # r >= n -> 0 -> reject
+            if seg:
+                tx.witness[i] = [sig, pub] if m != 13 else [sig, pub, b""]   # 13: 3 witness items
+            else:
+                tx.inputs[i].script = txgen.push(sig) + (txgen.push(pub) if pub else b"") + \
+                    (b"\x51" if m == 13 else b"")                        # 13: trailing OP_1
+            out_txs.append(sh.tx_serialize(tx))
+            out_jobs.append((len(out_txs) - 1, i, prev, val))
+            kinds.append(m)
+    return out_txs, out_jobs, kinds
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_std_inputs_records_and_verdicts_vs_oracle(torch, ver, coracle, forkid):
+    import hkv
+    rng = random.Random(31 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 5 != 0)) for k in range(16)]
+    txs, jobs = txgen.std_block(rng, 60, keys, forkid=forkid, p2wpkh_share=0.5, p2pk_share=0.2)
+    raw = [sh.tx_serialize(t) for t in txs]
+    mtx, mjobs, kinds = mutate_block(rng, txs, jobs, forkid)
+    all_raw = raw + mtx
+    all_jobs = jobs + [(t + len(raw), i, p, v) for (t, i, p, v) in mjobs]
+    recs = device_std_records(torch, ver, all_raw, all_jobs, forkid)
+    exp = b"".join(sh.std_input_record(sh.tx_parse(all_raw[t]), i, p, v, forkid) for (t, i, p, v) in all_jobs)
+    bad = [k for k in range(len(all_jobs)) if recs[k * 168:(k + 1) * 168] != exp[k * 168:(k + 1) * 168]]
+    assert not bad, [(k, kinds[k - len(jobs)] if k >= len(jobs) else "valid") for k in bad[:10]]
+    verdicts = hkv.verify_std_inputs(ver, all_raw, all_jobs, forkid)
+    want = oracle_batch(coracle, exp, 1)
+    assert verdicts == want.tolist()
+    assert all(verdicts[:len(jobs)])             # every generated input verifies
+    rej = [not v for v in verdicts[len(jobs):]]
+    assert sum(rej) > 0.8 * len(rej)             # nearly every mutation is rejected (oracle decides which)
+
+
+def test_std_inputs_bip143_example(ver):
+    import hkv
+    b = json.load(open(os.path.join(GOLDEN, "bip143_p2wpkh.json")))
+    tx = sh.tx_parse(bytes.fromhex(b["unsigned_tx"]))
+    i0, i1 = b["inputs"]
+    tx.inputs[0].script = txgen.push(bytes.fromhex(i0["sig"]))
+    tx.witness = [[], [bytes.fromhex(i1["sig"]), bytes.fromhex(i1["pubkey"])]]
+    raw = sh.tx_serialize(tx)
+    jobs = [(0, k, bytes.fromhex(x["script_pubkey"]), x["value"]) for k, x in enumerate(b["inputs"])]
+    assert hkv.verify_std_inputs(ver, [raw], jobs) == [True, True]
+    jobs_bad = [(0, k, s, v + 1) for (_, k, s, v) in jobs]
+    assert hkv.verify_std_inputs(ver, [raw], jobs_bad) == [True, False]  # only BIP143 commits to the amount
+
+
+def test_gen_keys_and_sign(torch, ver, coracle):
+    n = 300
+    priv = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    pub = torch.zeros(n * 33, dtype=torch.uint8, device="cuda")
+    h160 = torch.zeros(n * 20, dtype=torch.uint8, device="cuda")
+    ver.gen_keys_device(0, 99, n, priv.data_ptr(), pub.data_ptr(), h160.data_ptr())
+    msgs = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device="cuda")
+    idx = torch.arange(n, dtype=torch.int32, device="cuda").flip(0).contiguous()
+    sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    ver.gen_sign_device(0, 5, n, priv.data_ptr(), idx.data_ptr(), msgs.data_ptr(), 32, sig.data_ptr())
+    torch.cuda.synchronize()
+    P, Q, H, M, S = (x.cpu().numpy().tobytes() for x in (priv, pub, h160, msgs, sig))
+    recs = []
+    for k in range(n):
+        d = int.from_bytes(P[32 * k:32 * k + 32], "big")
+        pk = Q[33 * k:33 * k + 33]
+        assert o.pubkey_serialize(o.point_mul(d, o.G), True) == pk
+        assert sh.hash160(pk) == H[20 * k:20 * k + 20]
+        j = n - 1 - k  # signature j uses key idx[j] = n-1-j
+        recs.append(o.make_record(M[32 * j:32 * j + 32], S[64 * j:64 * j + 64], pk))
+    assert oracle_batch(coracle, b"".join(recs), 0).all()
