@@ -65,6 +65,50 @@ def cpu_baseline(records_host, threads: int):
             "single_thread_value": round(st_rate, 1), "sample_accepts": okm, "sample_n": nm}
 
 
+def block_mix(v, torch, sptr, steps: int) -> dict:
+    """BASELINE configs[2]: a 2,000-tx P2PKH + P2WPKH block verified end to
+    end on device (tx index, legacy / BIP143 sighash, DER + HASH160 template
+    checks, ECDSA) from HBM-resident tx bytes; plus the same pipeline on a
+    32-block batch (64,000 txs) for its throughput."""
+    from hkv import blockgen
+    out = {}
+    # a dedicated stream: torch's default stream is the null stream (pointer 0),
+    # which libhkv would replace by its own stream and the events would miss
+    bstream = torch.cuda.Stream()
+    sptr = bstream.cuda_stream
+    for label, n_tx in (("block", 2000), ("batch32", 64000)):
+        txs, inputs = blockgen.make_block(v, torch, n_tx=n_tx, seed=blockgen.SEED + n_tx)
+        db = blockgen.DeviceBlock(torch, txs, inputs)
+
+        def run():
+            v.verify_std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(),
+                                       db.bits.data_ptr(), sptr)
+
+        def extract():
+            v.std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(), sptr)
+
+        run()
+        torch.cuda.synchronize()
+        words = db.bits.cpu().numpy().view("uint32")
+        import numpy as np
+        accepted = int(np.unpackbits(words.view(np.uint8), bitorder="little")[:db.n].sum())
+        res = {"txs": n_tx, "inputs": db.n, "tx_bytes": int(db.d_bytes.numel()), "mismatches": db.n - accepted}
+        for name, fn in (("total", run), ("extract_sighash", extract)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            k = max(3, steps // (1 if label == "block" else 4))
+            e0.record(bstream)
+            for _ in range(k):
+                fn()
+            e1.record(bstream)
+            torch.cuda.synchronize()
+            res[f"{name}_us"] = round(e0.elapsed_time(e1) * 1e3 / k, 1)
+        res["inputs_per_s"] = round(db.n / (res["total_us"] * 1e-6), 1)
+        out[label] = res
+    out["workload"] = ("BASELINE configs[2]: 60% P2WPKH (BIP143) / 40% P2PKH (legacy) inputs, 1-3 inputs and 2 "
+                       "outputs per tx, SIGHASH_ALL; verifyStdInput semantics, tx bytes resident in HBM")
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,6 +117,7 @@ def main() -> None:
     ap.add_argument("--per-gpu", type=int, default=PER_GPU)
     ap.add_argument("--mode", type=int, default=0, help="0 = HKV_LIBSECP, 1 = HKV_HASKOIN")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-block-mix", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -98,7 +143,11 @@ def main() -> None:
     lo, hi = shard_bounds(n_total, rank, world)
     n = hi - lo
     v = hkv.Verifier(hkv.VerifierConfig(device_ids=[local]))
-    stream = torch.cuda.current_stream()
+    # a real (non-null) stream made current: libhkv enqueues on it and the RCCL
+    # all-gather, which waits on torch's current stream, is ordered after the
+    # verify (the null stream would not order against libhkv's own stream)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
     # each rank generates exactly its slice of the global synthetic batch
@@ -159,6 +208,9 @@ def main() -> None:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        mix = None
+        if world == 1 and not args.no_block_mix:
+            mix = block_mix(v, torch, sptr, args.steps)
         cpu = None
         if not args.no_cpu_baseline:
             host = recs[: min(n, 8192 * 16) * 168].cpu().numpy()
@@ -190,6 +242,7 @@ def main() -> None:
                          "kernel": "hkv_ecmult_kernel",
                          "products_per_verify": opcount.ECMULT_PRODUCTS_PER_VERIFY},
             "cpu_baseline": cpu,
+            "block_mix": mix,
         }
         print(json.dumps(line), flush=True)
     v.close()

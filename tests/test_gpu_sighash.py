@@ -254,3 +254,19 @@ def test_gen_keys_and_sign(torch, ver, coracle):
         j = n - 1 - k  # signature j uses key idx[j] = n-1-j
         recs.append(o.make_record(M[32 * j:32 * j + 32], S[64 * j:64 * j + 64], pk))
     assert oracle_batch(coracle, b"".join(recs), 0).all()
+
+
+def test_block_mix_config3_all_valid(torch, ver, coracle):
+    """BASELINE configs[2]: 2,000-tx P2PKH + P2WPKH block from the product-side
+    generator verifies end to end; a sample is re-derived by the oracle."""
+    import hkv
+    from hkv import blockgen
+    txs, inputs = blockgen.make_block(ver, torch, n_tx=2000)
+    assert 3000 < len(inputs) < 5000
+    got = hkv.verify_std_inputs(ver, txs, inputs)
+    assert all(got)
+    sample = inputs[::37]
+    recs = device_std_records(torch, ver, txs, sample, None)
+    exp = b"".join(sh.std_input_record(sh.tx_parse(txs[t]), i, p, v) for (t, i, p, v) in sample)
+    assert recs == exp
+    assert oracle_batch(coracle, exp, 1).all()
