@@ -109,6 +109,36 @@ def block_mix(v, torch, sptr, steps: int) -> dict:
     return out
 
 
+def adversarial_mix(v, torch, recs, n: int, sptr: int, steps: int) -> dict:
+    """BASELINE configs[3]: the timed batch with 30% of its records mutated into
+    the SURVEY §8(c) invalid classes (hkv/adversarial.py: labels fixed by
+    construction), verified in both modes; mismatches must be 0."""
+    import numpy as np
+    from hkv import adversarial
+    adv, lab_lib, lab_hask, _ = adversarial.mutate(recs.cpu().numpy(), seed=0x484B5634)
+    d = torch.from_numpy(adv).to(recs.device)
+    words = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device=recs.device)
+    stream = torch.cuda.current_stream()
+    out = {"records": n, "invalid_frac": round(float(1 - lab_lib.mean()), 4)}
+    for name, mode, lab in (("libsecp", 0, lab_lib), ("haskoin", 1, lab_hask)):
+        v.verify_device(0, d.data_ptr(), n, mode, words.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        got = adversarial.unpack_bits(words.cpu().numpy().view(np.uint32), n)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k = max(3, steps // 2)
+        e0.record(stream)
+        for _ in range(k):
+            v.verify_device(0, d.data_ptr(), n, mode, words.data_ptr(), sptr)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / k
+        out[name] = {"mismatches": int((got != lab).sum()), "accepts": int(got.sum()),
+                     "ms": round(ms, 4), "verifies_per_s": round(n / (ms * 1e-3), 1)}
+    out["workload"] = ("BASELINE configs[3]: msg-bit / r=0 / s>=n / bad prefix / x>=p / high-S mutations of "
+                       "the config-2 records, labels by construction")
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,6 +148,7 @@ def main() -> None:
     ap.add_argument("--mode", type=int, default=0, help="0 = HKV_LIBSECP, 1 = HKV_HASKOIN")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-block-mix", action="store_true")
+    ap.add_argument("--no-adversarial", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -211,6 +242,9 @@ def main() -> None:
         mix = None
         if world == 1 and not args.no_block_mix:
             mix = block_mix(v, torch, sptr, args.steps)
+        adv = None
+        if world == 1 and not args.no_adversarial:
+            adv = adversarial_mix(v, torch, recs, n, sptr, args.steps)
         cpu = None
         if not args.no_cpu_baseline:
             host = recs[: min(n, 8192 * 16) * 168].cpu().numpy()
@@ -243,6 +277,7 @@ def main() -> None:
                          "products_per_verify": opcount.ECMULT_PRODUCTS_PER_VERIFY},
             "cpu_baseline": cpu,
             "block_mix": mix,
+            "adversarial": adv,
         }
         print(json.dumps(line), flush=True)
     v.close()

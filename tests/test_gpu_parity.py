@@ -265,3 +265,55 @@ def test_batch_api_pinned_buffer(ver, kat):
         assert lib.hkv_verify(ver.ctx, b, len(recs) + 1, 1, words) == -1  # over capacity
     finally:
         lib.hkv_batch_free(b)
+
+
+def verify_dev_bits(torch, ver, d, n, mode, offset=0):
+    words = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    ver.verify_device(0, d.data_ptr() + offset * 168, n, mode, words.data_ptr())
+    torch.cuda.synchronize()
+    return words.cpu().numpy().view(np.uint32)
+
+
+def test_config4_adversarial_1m_both_modes(torch, ver, coracle):
+    """BASELINE configs[3]: 1,048,576 records, 30% invalid over the §8(c)
+    classes, exact reject parity in both modes against the construction labels
+    (hkv/adversarial.py, pinned per class by test_adversarial_labels.py) and a
+    32k slice against the C oracle."""
+    from hkv import adversarial
+    n = 1 << 20
+    d = gen_device(torch, ver, n, seed=0x484B5634)
+    adv, lab_lib, lab_hask, cls = adversarial.mutate(d.cpu().numpy(), seed=0x484B5634)
+    assert 0.29 < (cls >= 0).mean() < 0.31
+    d.copy_(torch.from_numpy(adv))
+    for mode, lab in ((0, lab_lib), (1, lab_hask)):
+        got = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n, mode), n)
+        mism = np.nonzero(got != lab)[0]
+        assert mism.size == 0, (mode, mism[:10], cls[mism[:10]])
+        sl = slice(500_000 * 168, (500_000 + 32768) * 168)
+        exp = oracle_batch(coracle, adv[sl].tobytes(), mode, threads=16)
+        assert (got[500_000:500_000 + 32768] == exp).all()
+
+
+def test_config5_ibd_16m_sharded_bitmap(torch, ver):
+    """BASELINE configs[4] shape on one GPU: 16,777,216 records (config-2
+    distribution, 5% invalid), verified as the 8 contiguous shards of the
+    8-GPU run (hkv/shard.py) and assembled as the all-gather does; the bitmap
+    equals the single-launch bitmap and the construction labels bit for bit."""
+    from hkv import adversarial
+    from hkv.shard import assemble_bitmap, shard_bounds
+    n, world = 1 << 24, 8
+    d = gen_device(torch, ver, n, seed=0x484B5635)
+    adv, lab, _, _ = adversarial.mutate(d.cpu().numpy(), seed=0x484B5635, invalid_frac=0.05)
+    d.copy_(torch.from_numpy(adv))
+    del adv
+    whole = verify_dev_bits(torch, ver, d, n, 0)[: (n + 31) // 32]
+    wpr = (n // world + 63) // 64 * 2 + 2
+    gathered = np.zeros(world * wpr, dtype=np.uint32)
+    for r in range(world):
+        lo, hi = shard_bounds(n, r, world)
+        w = verify_dev_bits(torch, ver, d, hi - lo, 0, offset=lo)
+        gathered[r * wpr: r * wpr + w.size] = w
+    full = assemble_bitmap(n, world, gathered, wpr)
+    assert (full == whole).all()
+    got = adversarial.unpack_bits(full, n)
+    assert (got == lab).all(), np.nonzero(got != lab)[0][:10]
