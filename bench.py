@@ -109,6 +109,55 @@ def block_mix(v, torch, sptr, steps: int) -> dict:
     return out
 
 
+def header_batches(v, torch, steps: int) -> dict:
+    """importHeaders' per-header work (headerHash +
+    isValidPOW + linkage) for a 2,000-header peer message (a chained bchRegTest
+    batch, hashed on the host with hashlib to build the links) and for 1M
+    HBM-resident random headers (throughput)."""
+    import hashlib
+    import numpy as np
+    from hkv import headers as hh
+    limit = (1 << 255) - 1  # bchRegTest powLimit
+    rng = np.random.default_rng(0x48445231)
+    out = {}
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    for label, n in (("message2000", 2000), ("batch1m", 1 << 20)):
+        raw = rng.integers(0, 256, size=(n, 80), dtype=np.uint8)
+        raw[:, 72:76] = np.frombuffer((0x207FFFFF).to_bytes(4, "little"), dtype=np.uint8)
+        if label == "message2000":
+            for i in range(1, n):
+                raw[i, 4:36] = np.frombuffer(hashlib.sha256(hashlib.sha256(raw[i - 1].tobytes()).digest()).digest(),
+                                             dtype=np.uint8)
+        d = torch.from_numpy(raw.reshape(-1)).cuda()
+        lim = torch.from_numpy(np.frombuffer(limit.to_bytes(32, "little"), dtype=np.uint8).copy()).cuda()
+        hashes = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+
+        def run():
+            hh.check_headers_device(v, 0, d.data_ptr(), n, lim.data_ptr(), None, hashes.data_ptr(),
+                                    status.data_ptr(), sp)
+        run()
+        torch.cuda.synchronize()
+        st = status.cpu().numpy()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k = max(5, steps)
+        e0.record(stream)
+        for _ in range(k):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / k
+        res = {"headers": n, "us": round(us, 1), "headers_per_s": round(n / (us * 1e-6), 1),
+               "pow_ok": int((st & hh.HKV_HDR_POW_OK).astype(bool).sum())}
+        if label == "message2000":
+            res["linked"] = int((st & hh.HKV_HDR_LINK_OK).astype(bool).sum())
+        out[label] = res
+    out["workload"] = ("SURVEY §8(f) rank 4: importHeaders (Chain.hs:500-520) headerHash + isValidPOW + prev "
+                       "linkage, bchRegTest bits 0x207fffff, headers resident in HBM")
+    return out
+
+
 def adversarial_mix(v, torch, recs, n: int, sptr: int, steps: int) -> dict:
     """BASELINE configs[3]: the timed batch with 30% of its records mutated into
     the SURVEY §8(c) invalid classes (hkv/adversarial.py: labels fixed by
@@ -149,6 +198,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-block-mix", action="store_true")
     ap.add_argument("--no-adversarial", action="store_true")
+    ap.add_argument("--no-headers", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -242,6 +292,9 @@ def main() -> None:
         mix = None
         if world == 1 and not args.no_block_mix:
             mix = block_mix(v, torch, sptr, args.steps)
+        hdr = None
+        if world == 1 and not args.no_headers:
+            hdr = header_batches(v, torch, args.steps)
         adv = None
         if world == 1 and not args.no_adversarial:
             adv = adversarial_mix(v, torch, recs, n, sptr, args.steps)
@@ -278,6 +331,7 @@ def main() -> None:
             "cpu_baseline": cpu,
             "block_mix": mix,
             "adversarial": adv,
+            "headers": hdr,
         }
         print(json.dumps(line), flush=True)
     v.close()

@@ -44,8 +44,9 @@ struct DevCtx {
   // tx index rows (hkv_sighash.hip) and host-API staging buffers
   uint32_t* txt = nullptr;
   size_t txt_cap = 0;  // bytes
-  void* stage[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  size_t stage_cap[5] = {0, 0, 0, 0, 0};
+  // [0..3] tx batch, [4] sighash out, [5] header batch
+  void* stage[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t stage_cap[6] = {0, 0, 0, 0, 0, 0};
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -614,4 +615,46 @@ int hkv_gen_sign_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, const ui
   return HKV_OK;
 }
 
+static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+int hkv_check_headers_device(hkv_ctx* ctx, int dev, const uint8_t* d_headers, size_t n, const uint8_t* d_pow_limit,
+                             const uint8_t* d_prev_hash, uint8_t* d_hashes, uint8_t* d_status, void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!d_headers || !d_pow_limit || !d_hashes || !d_status || !aligned(d_headers, 4) || !aligned(d_pow_limit, 4) ||
+      !aligned(d_prev_hash, 4) || !aligned(d_hashes, 16))
+    return HKV_E_ARG;
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  HKV_TRY(hkv::launch_headers(d_headers, (uint32_t)n, d_pow_limit, d_prev_hash, d_hashes, d_status, st),
+          "headers launch");
+  return HKV_OK;
+}
+
+int hkv_check_headers(hkv_ctx* ctx, const uint8_t* headers, size_t n, const uint8_t* pow_limit,
+                      const uint8_t* prev_hash, uint8_t* hashes_out, uint8_t* status) {
+  if (!ctx || ctx->devs.empty() || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (n == 0) return HKV_OK;
+  if (!headers || !pow_limit || !hashes_out || !status) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[0];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  // one staging buffer: limit (32) | prev (32) | headers (n*80) | hashes (n*32) | status (n)
+  int rc = grow(&d.stage[5], &d.stage_cap[5], 64 + n * 113, "hipMalloc(header batch)");
+  if (rc) return rc;
+  uint8_t* b = static_cast<uint8_t*>(d.stage[5]);
+  uint8_t *dlim = b, *dprev = b + 32, *dh = b + 64, *dhash = dh + n * 80, *dst = dhash + n * 32;
+  HKV_TRY(hipMemcpyAsync(dlim, pow_limit, 32, hipMemcpyHostToDevice, d.stream), "H2D pow limit");
+  if (prev_hash) HKV_TRY(hipMemcpyAsync(dprev, prev_hash, 32, hipMemcpyHostToDevice, d.stream), "H2D prev");
+  HKV_TRY(hipMemcpyAsync(dh, headers, n * 80, hipMemcpyHostToDevice, d.stream), "H2D headers");
+  HKV_TRY(hkv::launch_headers(dh, (uint32_t)n, dlim, prev_hash ? dprev : nullptr, dhash, dst, d.stream),
+          "headers launch");
+  HKV_TRY(hipMemcpyAsync(hashes_out, dhash, n * 32, hipMemcpyDeviceToHost, d.stream), "D2H header hashes");
+  HKV_TRY(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, d.stream), "D2H header status");
+  HKV_TRY(hipStreamSynchronize(d.stream), "headers sync");
+  return HKV_OK;
+}
+
 }  // extern "C"
+

@@ -1,0 +1,149 @@
+// hkv_headers.hip — batch block-header checks.
+//
+// The data-parallel part of haskoin-node's header sync: importHeaders
+// (/root/reference/src/Haskoin/Node/Chain.hs:500-520) hands each peer's
+// `headers` message (up to 2,000 headers) to haskoin-core connectBlocks
+// [dep, haskoin-core-1.1.0, stack.yaml:10], which for every header computes
+// headerHash (SHA-256d of the 80-byte wire form) and checks isValidPOW and
+// that the header extends its predecessor. Those three are independent per
+// header and run here, one lane per header:
+//
+//   hkv_header_hash_kernel  SHA-256d (2 + 1 compressions), decodeCompact of
+//                           the bits field, isValidPOW against powLimit.
+//   hkv_header_link_kernel  prev field of header i == hash of header i-1
+//                           (header 0 against the caller's tip hash).
+//
+// Memory: a workgroup's 256 headers (20,480 contiguous bytes) are staged into
+// LDS by coalesced dword loads, then each lane reads its own 20 words. The
+// work is 3 SHA-256 compressions per 80-byte header: latency- and ALU-light,
+// far below both the VALU and HBM rooflines at sync batch sizes (a 2,000-
+// header message is 160 KB); DESIGN.md records the measured rate.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hkv_hash.h"
+#include "hkv_layout.h"
+#include "hkv_internal.h"
+#include "../../include/hkv.h"
+
+namespace hkv {
+
+constexpr int HDR_WORDS = 20;  // 80 bytes
+
+// haskoin-core decodeCompact (Haskoin.Block.Common) [dep]: the Bitcoin
+// "compact" target. Writes the target as 8 little-endian limbs when it does
+// not overflow. Returns the HKV_HDR_{NEGATIVE,OVERFLOW,ZERO_TARGET} flags.
+HKV_DEV uint32_t decode_compact(uint32_t bits, uint32_t t[8]) {
+  const uint32_t size = bits >> 24;
+  const uint32_t w0 = bits & 0x007FFFFFu;
+  const uint32_t word = size <= 3 ? (w0 >> (8 * (3 - size))) : w0;
+  uint32_t fl = 0;
+  if (word != 0 && (bits & 0x00800000u)) fl |= HKV_HDR_NEGATIVE;
+  if (word != 0 && (size > 34 || (word > 0xFFu && size > 33) || (word > 0xFFFFu && size > 32)))
+    fl |= HKV_HDR_OVERFLOW;
+  if (word == 0) fl |= HKV_HDR_ZERO_TARGET;
+  // value = word << 8*(size-3) (size > 3); fits 256 bits whenever !overflow
+  const uint32_t s = size > 3 ? 8u * (size - 3u) : 0u;
+  const uint64_t v = (uint64_t)word << (s & 31u);
+  const uint32_t li = s >> 5;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = ((uint32_t)j == li) ? (uint32_t)v : ((uint32_t)j == li + 1) ? (uint32_t)(v >> 32) : 0u;
+  return fl;
+}
+
+// a > b for 8-limb little-endian integers
+HKV_DEV bool u256_gt(const uint32_t a[8], const uint32_t b[8]) {
+  bool gt = false, decided = false;
+#pragma unroll
+  for (int j = 7; j >= 0; --j) {
+    gt = decided ? gt : (a[j] > b[j]);
+    decided = decided || (a[j] != b[j]);
+  }
+  return gt;
+}
+
+__global__ void __launch_bounds__(WG) hkv_header_hash_kernel(const uint32_t* __restrict__ hdrs, uint32_t n,
+                                                             const uint32_t* __restrict__ pow_limit,
+                                                             uint32_t* __restrict__ hashes,
+                                                             uint8_t* __restrict__ status) {
+  __shared__ uint32_t lds[WG * HDR_WORDS];
+  const uint32_t base = blockIdx.x * WG;
+  const uint32_t cnt = min((uint32_t)WG, n - base);
+  const uint32_t* src = hdrs + (size_t)base * HDR_WORDS;
+  for (uint32_t k = threadIdx.x; k < cnt * HDR_WORDS; k += WG) lds[k] = src[k];
+  __syncthreads();
+  const uint32_t i = base + threadIdx.x;
+  if (threadIdx.x >= cnt) return;
+  uint32_t h[HDR_WORDS];
+#pragma unroll
+  for (int k = 0; k < HDR_WORDS; ++k) h[k] = lds[threadIdx.x * HDR_WORDS + k];
+
+  // SHA-256 of the 80 bytes: block 1 = words 0..15, block 2 = words 16..19 + padding
+  uint32_t st[8], w[16];
+  sha256_init(st);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = __builtin_bswap32(h[k]);
+  sha256_compress(st, w);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = __builtin_bswap32(h[16 + k]);
+  w[4] = 0x80000000u;
+#pragma unroll
+  for (int k = 5; k < 15; ++k) w[k] = 0;
+  w[15] = 640;
+  sha256_compress(st, w);
+  uint32_t d[8];
+  sha256_of_digest(d, st);
+
+  // headerHash bytes in digest order == little-endian limbs of headerPOW
+  uint32_t hv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) hv[k] = __builtin_bswap32(d[k]);
+  uint32_t* out = hashes + (size_t)i * 8;
+#pragma unroll
+  for (int k = 0; k < 8; k += 4) *reinterpret_cast<uint4*>(out + k) = make_uint4(hv[k], hv[k + 1], hv[k + 2], hv[k + 3]);
+
+  // isValidPOW
+  uint32_t tgt[8], lim[8];
+  uint32_t fl = decode_compact(h[18], tgt);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) lim[k] = pow_limit[k];
+  if (!(fl & HKV_HDR_OVERFLOW)) {
+    if (u256_gt(tgt, lim)) fl |= HKV_HDR_ABOVE_LIMIT;
+    if (u256_gt(hv, tgt)) fl |= HKV_HDR_HASH_ABOVE;
+  }
+  if (!(fl & (HKV_HDR_NEGATIVE | HKV_HDR_OVERFLOW | HKV_HDR_ZERO_TARGET | HKV_HDR_ABOVE_LIMIT | HKV_HDR_HASH_ABOVE)))
+    fl |= HKV_HDR_POW_OK;
+  status[i] = (uint8_t)fl;
+}
+
+// prev field (words 1..8) of header i against the hash of header i-1
+__global__ void __launch_bounds__(WG) hkv_header_link_kernel(const uint32_t* __restrict__ hdrs, uint32_t n,
+                                                             const uint32_t* __restrict__ prev0,
+                                                             const uint32_t* __restrict__ hashes,
+                                                             uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* p = hdrs + (size_t)i * HDR_WORDS + 1;
+  const uint32_t* q = i ? hashes + (size_t)(i - 1) * 8 : prev0;
+  uint32_t diff = 0;
+  if (q) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) diff |= p[k] ^ q[k];
+  }
+  if (diff == 0) status[i] = (uint8_t)(status[i] | HKV_HDR_LINK_OK);
+}
+
+hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
+                          uint8_t* hashes, uint8_t* status, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint32_t blocks = (n + WG - 1) / WG;
+  hipLaunchKernelGGL(hkv_header_hash_kernel, dim3(blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(hdrs),
+                     n, reinterpret_cast<const uint32_t*>(pow_limit), reinterpret_cast<uint32_t*>(hashes), status);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hkv_header_link_kernel, dim3(blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(hdrs),
+                     n, reinterpret_cast<const uint32_t*>(prev0), reinterpret_cast<const uint32_t*>(hashes), status);
+  return hipGetLastError();
+}
+
+}  // namespace hkv

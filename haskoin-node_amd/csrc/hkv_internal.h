@@ -48,4 +48,7 @@ hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt
 hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                              uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                              uint8_t* recs, hipStream_t st);
+// hkv_headers.hip
+hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
+                          uint8_t* hashes, uint8_t* status, hipStream_t st);
 }  // namespace hkv

@@ -8,6 +8,7 @@ and fails loudly when it is missing. There is no CPU fallback.
 from .lib import (HKV_HASKOIN, HKV_LIBSECP, HKV_NO_FORKID, HKV_RECORD_SIZE, HKV_SIGHASH_FORKID,
                   HKV_SIGHASH_LEGACY, HkvError, HkvTxs, lib_path, load_library)
 from .records import make_record, pack_records, unpack_bits
+from .headers import check_headers, check_headers_device
 from .sighash import TxBatch, tx_sig_hash_batch, verify_std_inputs
 from .verify import (Verifier, VerifierConfig, verify_hash_sig_batch,
                      verify_raw_batch)
@@ -17,5 +18,5 @@ __all__ = [
     "load_library", "make_record", "pack_records", "unpack_bits", "Verifier",
     "VerifierConfig", "verify_hash_sig_batch", "verify_raw_batch", "HKV_NO_FORKID",
     "HKV_SIGHASH_FORKID", "HKV_SIGHASH_LEGACY", "HkvTxs", "TxBatch", "tx_sig_hash_batch",
-    "verify_std_inputs",
+    "verify_std_inputs", "check_headers", "check_headers_device",
 ]

@@ -16,6 +16,9 @@ HKV_SIGHASH_FORKID = 1
 HKV_NO_FORKID = -1
 HKV_SH_OK, HKV_SH_BAD_TX, HKV_SH_BAD_INPUT, HKV_SH_BAD_REF = 0, 1, 2, 3
 
+HKV_HDR_POW_OK, HKV_HDR_LINK_OK, HKV_HDR_NEGATIVE, HKV_HDR_OVERFLOW = 0x01, 0x02, 0x04, 0x08
+HKV_HDR_ZERO_TARGET, HKV_HDR_ABOVE_LIMIT, HKV_HDR_HASH_ABOVE = 0x10, 0x20, 0x40
+
 HKV_OK = 0
 _ERRS = {-1: "HKV_E_ARG", -2: "HKV_E_NODEV", -3: "HKV_E_OOM", -4: "HKV_E_HIP", -5: "HKV_E_INTERNAL"}
 
@@ -80,6 +83,9 @@ EXPORTS = {
                                              c_void_p, c_void_p, c_void_p]),
     "hkv_verify_std_inputs": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
                                       POINTER(c_uint32)]),
+    "hkv_check_headers": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hkv_check_headers_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p]),
     "hkv_gen_keys_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hkv_gen_sign_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_void_p, c_void_p, c_void_p, c_size_t,
                                     c_void_p, c_void_p]),

@@ -190,6 +190,37 @@ int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, co
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
                           uint32_t* verdict_bits);
 
+/* ---------------------------------------------------------------------------
+ * Header batches: the data-parallel part of
+ * importHeaders (/root/reference/src/Haskoin/Node/Chain.hs:500-520), which
+ * hands up to 2,000 headers per peer message to haskoin-core connectBlocks
+ * [dep]. Per header: headerHash (SHA-256d of the 80-byte wire form) and
+ * isValidPOW net h = target > 0 && !overflow && target <= powLimit &&
+ * headerPOW h <= target, with (target, overflow) = decodeCompact h.bits;
+ * plus the batch linkage connectBlocks relies on (prev field of header i
+ * == headerHash of header i-1). The chain-context checks (median time past,
+ * retarget / nextWorkRequired, checkpoints, BIP34) stay on the host.
+ * ------------------------------------------------------------------------ */
+#define HKV_HDR_POW_OK 0x01u           /* isValidPOW                               */
+#define HKV_HDR_LINK_OK 0x02u          /* prev == hash of the previous header      */
+#define HKV_HDR_NEGATIVE 0x04u         /* decodeCompact sign bit with nonzero word */
+#define HKV_HDR_OVERFLOW 0x08u         /* decodeCompact overflow                   */
+#define HKV_HDR_ZERO_TARGET 0x10u      /* target == 0                              */
+#define HKV_HDR_ABOVE_LIMIT 0x20u      /* target > powLimit                        */
+#define HKV_HDR_HASH_ABOVE 0x40u       /* headerPOW > target                       */
+
+/* headers: n * 80 wire bytes. pow_limit: 32 bytes, little-endian integer
+ * (the network's powLimit). prev_hash: 32 bytes in internal (digest) order,
+ * the hash header 0 must extend, or NULL (header 0 then counts as linked).
+ * hashes_out: n * 32 bytes (digest order, i.e. headerHash's serialisation);
+ * status: n bytes of HKV_HDR_* flags. Host memory, first device, blocking. */
+int hkv_check_headers(hkv_ctx* ctx, const uint8_t* headers, size_t n, const uint8_t* pow_limit,
+                      const uint8_t* prev_hash, uint8_t* hashes_out, uint8_t* status);
+/* Device form: every pointer in HBM of device `dev`; enqueued on hip_stream,
+ * not synchronised. */
+int hkv_check_headers_device(hkv_ctx* ctx, int dev, const uint8_t* d_headers, size_t n, const uint8_t* d_pow_limit,
+                             const uint8_t* d_prev_hash, uint8_t* d_hashes, uint8_t* d_status, void* hip_stream);
+
 /* Synthetic-data hooks (block-mix generator, off the verify path):
  * n random private keys -> d_priv (n*32, big-endian), compressed public keys
  * d_pub (n*33) and their HASH160 d_h160 (n*20);
