@@ -11,6 +11,7 @@ Errors follow the ABI: a verdict is never an error; a device failure raises
 from __future__ import annotations
 
 import ctypes
+import sys
 from dataclasses import dataclass, field
 from typing import Iterable, List, Optional, Sequence, Tuple
 
@@ -32,6 +33,15 @@ class Verifier:
 
     def __init__(self, config: VerifierConfig | None = None):
         self.lib = load_library()
+        # PyTorch-ROCm bundles its own HIP runtime; if libhkv's runtime (from
+        # /opt/rocm) claims the device first, torch's later init finds no GPU.
+        # When the caller already uses torch, initialise it first.
+        tmod = sys.modules.get("torch")
+        if tmod is not None:
+            try:
+                tmod.cuda.init()
+            except Exception:  # pragma: no cover - no GPU / CPU-only torch
+                pass
         self.config = config or VerifierConfig()
         ctx = ctypes.c_void_p()
         if self.config.device_ids is None:

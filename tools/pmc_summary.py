@@ -25,6 +25,23 @@ def main(src: str, dst: str) -> None:
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    # per (kernel, grid) launch durations from the kernel trace: the ecmult
+    # grid is fixed (grid-stride), so the median is the 1M-record launch and
+    # the open-time self-check launch does not skew it
+    traces = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))
+    if traces:
+        durs = defaultdict(list)
+        for r in csv.DictReader(open(traces[0])):
+            k = r["Kernel_Name"].split("(")[0].replace("hkv::", "")
+            g = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
+            durs[(k, g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        ks = {}
+        for (k, g), v in sorted(durs.items()):
+            v.sort()
+            ks[f"{k}@grid{g}"] = {"calls": len(v), "avg_us": round(sum(v) / len(v), 2),
+                                  "median_us": round(v[len(v) // 2], 2), "min_us": round(v[0], 2),
+                                  "max_us": round(v[-1], 2)}
+        json.dump(ks, open(os.path.join(dst, "kernel_by_grid.json"), "w"), indent=1)
     per = defaultdict(lambda: defaultdict(list))
     grid = {}
     for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
@@ -35,7 +52,7 @@ def main(src: str, dst: str) -> None:
                 continue
             per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             grid[k] = g
-    out = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in per.items()}
+    out = {k: {c: sorted(v)[len(v) // 2] for c, v in d.items()} for k, d in per.items()}  # median launch
     for k in out:
         out[k]["Grid_Size"] = grid[k]
     json.dump(out, open(os.path.join(dst, "pmc.json"), "w"), indent=1)
