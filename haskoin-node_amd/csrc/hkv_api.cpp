@@ -419,7 +419,7 @@ int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, ui
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = enqueue_verify(d, d_records, n, mode, st);
   if (rc) return rc;
   const size_t words = (n + 31) / 32;
@@ -436,7 +436,7 @@ int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint3
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = ensure_pool(d, seed ^ 0x706F6F6Cull, pool_size, st);
   if (rc) return rc;
   HKV_TRY(hkv::launch_gen_records(seed, (uint32_t)n, d.pool, d.pool_n, uncompressed_permille, d_records, st),
@@ -450,7 +450,7 @@ int hkv_debug_op(hkv_ctx* ctx, int dev, uint32_t op, size_t n, const uint32_t* d
   if (n == 0) return HKV_OK;
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   HKV_TRY(hkv::launch_debug(op, (uint32_t)n, d_a, d_b, d_out, st), "debug launch");
   return HKV_OK;
 }
@@ -499,7 +499,7 @@ int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_si
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = enqueue_tx_index(d, d_txs, st);
   if (rc) return rc;
   HKV_TRY(hkv::launch_sighash(d_txs->bytes, d_txs->n_tx, d.txt, d_txs->scripts, d_txs->scripts_len, d_jobs,
@@ -541,7 +541,7 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   return enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
 }
 
@@ -553,7 +553,7 @@ int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, co
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
   if (!rc) rc = enqueue_verify(d, d_records, n, HKV_MODE_HASKOIN, st);
   if (rc) return rc;
@@ -594,7 +594,7 @@ int hkv_gen_keys_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint8_t*
   if (!d_priv || !d_pub || !d_h160) return HKV_E_ARG;
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   HKV_TRY(hkv::launch_gen_keys(seed, (uint32_t)n, d_priv, d_pub, d_h160, st), "gen keys launch");
   return HKV_OK;
 }
@@ -609,7 +609,7 @@ int hkv_gen_sign_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, const ui
   if (!d_priv || !d_msg || !d_sig) return HKV_E_ARG;
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   HKV_TRY(hkv::launch_gen_sign(seed, (uint32_t)n, d_priv, d_key_idx, d_msg, (uint32_t)msg_stride, d_sig, st),
           "gen sign launch");
   return HKV_OK;
@@ -626,7 +626,7 @@ int hkv_check_headers_device(hkv_ctx* ctx, int dev, const uint8_t* d_headers, si
     return HKV_E_ARG;
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-  hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : d.stream;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   HKV_TRY(hkv::launch_headers(d_headers, (uint32_t)n, d_pow_limit, d_prev_hash, d_hashes, d_status, st),
           "headers launch");
   return HKV_OK;

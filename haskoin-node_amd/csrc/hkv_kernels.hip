@@ -782,7 +782,11 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
                      (const uint32_t*)recs, n, n_pad, mode, im);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint32_t stride = ceil_div(n_pad, BATCH_INV);
+  // BATCH_INV signatures per lane at large n; small batches (a block) keep
+  // at least 65,536 lanes (or one per signature) so the latency of the
+  // sequential batch products does not dominate
+  uint32_t stride = ceil_div(n_pad, BATCH_INV);
+  stride = stride > 65536u ? stride : (n_pad < 65536u ? n_pad : 65536u);
   hipLaunchKernelGGL(hkv_inv_kernel, dim3(ceil_div(stride, WG)), dim3(WG), 0, st, n_pad, stride, im);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -1,0 +1,200 @@
+// hkv_safegcd.h — constant-time modular inversion mod the group order n by
+// Bernstein–Yang "safegcd" divsteps (Bernstein, Yang: "Fast constant-time
+// gcd computation and modular inversion", TCHES 2019), 30 divsteps per
+// matrix over signed radix-2^30 limbs.
+//
+// Replaces the Fermat chain a^(n-2) (≈ 255 squarings + 75 multiplications
+// mod n) used for s^-1 in secp256k1_ecdsa_sig_verify step (5) [dep; SURVEY.md
+// §8(a) a3]. The result is the same field element; only the cost changes:
+// 25 outer iterations × (30 branch-free divsteps on the low word, one 2×2
+// matrix applied to (f, g) and, mod n, to (d, e)).
+//
+// Bound: for odd f < 2^256 and 0 <= g < f, ⌊(49·256 + 80)/17⌋ = 742
+// divsteps (delta starting at 1) reach g = 0 (paper, Theorem 11.2); 25 × 30
+// = 750 are run. At that point f = ±1 and d·f ≡ g0^-1 (mod n).
+//
+// Limb form ("signed30"): limbs 0..7 hold 30 bits each in [0, 2^30), limb 8
+// is signed, value = Σ l_i 2^(30 i). d and e stay in (-2n, n).
+//
+// Written __host__ __device__ so the host build (tests/test_safegcd.py)
+// checks the same code the kernels run.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define HKV_HD __host__ __device__ __forceinline__
+#else
+#define HKV_HD static inline
+#endif
+
+namespace hkv {
+namespace sgcd {
+
+constexpr uint32_t M30 = 0x3FFFFFFFu;
+// n in signed30 limbs, and n^-1 mod 2^30
+constexpr int32_t NL[9] = {0x10364141, 0x3F497A33, 0x348A03BB, 0x2BB739AB, 0x3FFFFEBA,
+                           0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0xFFFF};
+constexpr uint32_t NINV30 = 0x2A774EC1u;
+
+// u256 (8 little-endian words) -> signed30
+HKV_HD void to30(int32_t r[9], const uint32_t a[8]) {
+  r[0] = (int32_t)(a[0] & M30);
+  r[1] = (int32_t)(((a[0] >> 30) | (a[1] << 2)) & M30);
+  r[2] = (int32_t)(((a[1] >> 28) | (a[2] << 4)) & M30);
+  r[3] = (int32_t)(((a[2] >> 26) | (a[3] << 6)) & M30);
+  r[4] = (int32_t)(((a[3] >> 24) | (a[4] << 8)) & M30);
+  r[5] = (int32_t)(((a[4] >> 22) | (a[5] << 10)) & M30);
+  r[6] = (int32_t)(((a[5] >> 20) | (a[6] << 12)) & M30);
+  r[7] = (int32_t)(((a[6] >> 18) | (a[7] << 14)) & M30);
+  r[8] = (int32_t)(a[7] >> 16);
+}
+
+// 30 divsteps on the low words of f and g; returns the transition matrix
+// (u, v, q, r) scaled by 2^30 and the updated delta.
+HKV_HD int32_t divsteps30(int32_t delta, uint32_t f, uint32_t g, int32_t t[4]) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+  for (int i = 0; i < 30; ++i) {
+    // delta > 0 and g odd: (f, g, u, v, q, r, delta) <- (g, -f, q, r, -u, -v, -delta)
+    const uint32_t sw = (uint32_t)(-(int32_t)((delta > 0) & (int32_t)(g & 1u)));
+    const uint32_t f0 = f, u0 = u, v0 = v;
+    f = (g & sw) | (f & ~sw);
+    g = ((0u - f0) & sw) | (g & ~sw);
+    u = (q & sw) | (u & ~sw);
+    q = ((0u - u0) & sw) | (q & ~sw);
+    v = (r & sw) | (v & ~sw);
+    r = ((0u - v0) & sw) | (r & ~sw);
+    delta = (int32_t)(((uint32_t)(-delta) & sw) | ((uint32_t)delta & ~sw));
+    // g odd: g += f, q += u, r += v
+    const uint32_t od = 0u - (g & 1u);
+    g += f & od;
+    q += u & od;
+    r += v & od;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+    delta += 1;
+  }
+  t[0] = (int32_t)u;
+  t[1] = (int32_t)v;
+  t[2] = (int32_t)q;
+  t[3] = (int32_t)r;
+  return delta;
+}
+
+// (f, g) <- t (f, g) / 2^30 (exact)
+HKV_HD void update_fg(int32_t f[9], int32_t g[9], const int32_t t[4]) {
+  const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+  int64_t cf = u * f[0] + v * g[0];
+  int64_t cg = q * f[0] + r * g[0];
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; ++i) {
+    cf += u * f[i] + v * g[i];
+    cg += q * f[i] + r * g[i];
+    f[i - 1] = (int32_t)((uint32_t)cf & M30);
+    g[i - 1] = (int32_t)((uint32_t)cg & M30);
+    cf >>= 30;
+    cg >>= 30;
+  }
+  f[8] = (int32_t)cf;
+  g[8] = (int32_t)cg;
+}
+
+// (d, e) <- t (d, e) / 2^30 (mod n), adding multiples of n to make the
+// division exact; keeps d, e in (-2n, n).
+HKV_HD void update_de(int32_t d[9], int32_t e[9], const int32_t t[4]) {
+  const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
+  const int32_t sd = d[8] >> 31, se = e[8] >> 31;
+  int32_t md = (u & sd) + (v & se);
+  int32_t me = (q & sd) + (r & se);
+  int64_t cd = (int64_t)u * d[0] + (int64_t)v * e[0];
+  int64_t ce = (int64_t)q * d[0] + (int64_t)r * e[0];
+  md -= (int32_t)((NINV30 * (uint32_t)cd + (uint32_t)md) & M30);
+  me -= (int32_t)((NINV30 * (uint32_t)ce + (uint32_t)me) & M30);
+  cd += (int64_t)NL[0] * md;
+  ce += (int64_t)NL[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; ++i) {
+    cd += (int64_t)u * d[i] + (int64_t)v * e[i] + (int64_t)NL[i] * md;
+    ce += (int64_t)q * d[i] + (int64_t)r * e[i] + (int64_t)NL[i] * me;
+    d[i - 1] = (int32_t)((uint32_t)cd & M30);
+    e[i - 1] = (int32_t)((uint32_t)ce & M30);
+    cd >>= 30;
+    ce >>= 30;
+  }
+  d[8] = (int32_t)cd;
+  e[8] = (int32_t)ce;
+}
+
+// r = a^-1 mod n for 0 < a < n (a = 0 gives 0).
+HKV_HD void inv_mod_n(uint32_t out[8], const uint32_t a[8]) {
+  int32_t f[9], g[9], d[9], e[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    f[i] = NL[i];
+    d[i] = 0;
+    e[i] = 0;
+  }
+  e[0] = 1;
+  to30(g, a);
+  int32_t delta = 1;
+#pragma unroll 1
+  for (int it = 0; it < 25; ++it) {
+    int32_t t[4];
+    delta = divsteps30(delta, (uint32_t)f[0] | ((uint32_t)f[1] << 30), (uint32_t)g[0] | ((uint32_t)g[1] << 30), t);
+    update_fg(f, g, t);
+    update_de(d, e, t);
+  }
+  // f = ±1: result = d * f, then into [0, n): d in (-2n, 2n)
+  const int32_t fneg = f[8] >> 31;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // d = fneg ? -d : d  (limb-wise, then renormalise)
+    c += (int64_t)((d[i] ^ fneg) - fneg);
+    d[i] = (int32_t)((uint32_t)c & M30);
+    c >>= 30;
+  }
+  d[8] = (int32_t)(c + ((d[8] ^ fneg) - fneg));
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {  // add n while negative
+    const int32_t neg = d[8] >> 31;
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (int64_t)d[i] + (NL[i] & neg);
+      d[i] = (int32_t)((uint32_t)c & M30);
+      c >>= 30;
+    }
+    d[8] = (int32_t)(c + d[8] + (NL[8] & neg));
+  }
+  {  // subtract n once if d >= n: compute d - n, keep it when non-negative
+    int32_t s[9];
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (int64_t)d[i] - NL[i];
+      s[i] = (int32_t)((uint32_t)c & M30);
+      c >>= 30;
+    }
+    s[8] = (int32_t)(c + d[8] - NL[8]);
+    const int32_t keep = ~(s[8] >> 31);  // all ones when d - n >= 0
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d[i] = (s[i] & keep) | (d[i] & ~keep);
+  }
+  // signed30 (now in [0, n)) -> 8 words
+  out[0] = (uint32_t)d[0] | ((uint32_t)d[1] << 30);
+  out[1] = ((uint32_t)d[1] >> 2) | ((uint32_t)d[2] << 28);
+  out[2] = ((uint32_t)d[2] >> 4) | ((uint32_t)d[3] << 26);
+  out[3] = ((uint32_t)d[3] >> 6) | ((uint32_t)d[4] << 24);
+  out[4] = ((uint32_t)d[4] >> 8) | ((uint32_t)d[5] << 22);
+  out[5] = ((uint32_t)d[5] >> 10) | ((uint32_t)d[6] << 20);
+  out[6] = ((uint32_t)d[6] >> 12) | ((uint32_t)d[7] << 18);
+  out[7] = ((uint32_t)d[7] >> 14) | ((uint32_t)d[8] << 16);
+}
+
+}  // namespace sgcd
+}  // namespace hkv

@@ -7,6 +7,7 @@
 // secp256k1_ecdsa_sig_verify [dep; SURVEY.md §8(a) a3, a5, a6].
 #pragma once
 #include "hkv_field.h"
+#include "hkv_safegcd.h"
 
 namespace hkv {
 
@@ -166,38 +167,10 @@ HKV_DEV void sc_sqr_n(sc& r, const sc& a, int n) {
   for (int i = 1; i < n; ++i) sc_sqr(r, r);
 }
 
-__constant__ static const uint32_t SC_INV_LOW[5] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u, 0u};
-
-// r = a^(n-2) = a^-1 (a != 0). n-2 = (2^127-1) << 129 | LOW129 with
-// LOW129 = 0x0_BAAEDCE6_AF48A03B_BFD25E8C_D036413F (bit 128 clear).
-HKV_DEV void sc_inv(sc& r, const sc& a) {
-  sc x2, x3, x6, x12, x24, x48, x96, x120, x126, t;
-  sc_sqr(x2, a);
-  sc_mul(x2, x2, a);
-  sc_sqr(x3, x2);
-  sc_mul(x3, x3, a);
-  sc_sqr_n(t, x3, 3);
-  sc_mul(x6, t, x3);
-  sc_sqr_n(t, x6, 6);
-  sc_mul(x12, t, x6);
-  sc_sqr_n(t, x12, 12);
-  sc_mul(x24, t, x12);
-  sc_sqr_n(t, x24, 24);
-  sc_mul(x48, t, x24);
-  sc_sqr_n(t, x48, 48);
-  sc_mul(x96, t, x48);
-  sc_sqr_n(t, x96, 24);
-  sc_mul(x120, t, x24);
-  sc_sqr_n(t, x120, 6);
-  sc_mul(x126, t, x6);
-  sc_sqr(t, x126);
-  sc_mul(t, t, a);  // x127
-  for (int bit = 128; bit >= 0; --bit) {
-    sc_sqr(t, t);
-    if ((SC_INV_LOW[bit >> 5] >> (bit & 31)) & 1u) sc_mul(t, t, a);  // wave-uniform branch
-  }
-  r = t;
-}
+// r = a^-1 mod n (0 < a < n; a = 0 gives 0): constant-time safegcd
+// (hkv_safegcd.h), ≈ 10x fewer VALU instructions than the Fermat chain
+// a^(n-2) it replaced (255 squarings + 75 multiplications mod n).
+HKV_DEV void sc_inv(sc& r, const sc& a) { sgcd::inv_mod_n(r.v, a.v); }
 
 HKV_DEV void sc_from_be_words(sc& r, const uint32_t w[8]) {
 #pragma unroll

@@ -31,6 +31,10 @@
  *       (Haskoin.Transaction.Builder) for P2PK / P2PKH / P2WPKH prevouts:
  *       decodeTxSig (strict DER, low S, hashtype), HASH160 check, sighash and
  *       verifyHashSig, all on device.
+ *   hkv_check_headers / hkv_check_headers_device
+ *       replaces the per-header part of haskoin-core `connectBlocks` reached
+ *       from importHeaders (/root/reference/src/Haskoin/Node/Chain.hs:500-520):
+ *       headerHash, isValidPOW (decodeCompact) and the prev-hash link.
  *
  * Conventions: no C++ exceptions cross this boundary; every function that
  * can fail returns 0 (HKV_OK) or a negative hkv_err. A verdict is never an
@@ -103,7 +107,9 @@ int hkv_verify_host(hkv_ctx* ctx, const uint8_t* records, size_t n, uint32_t mod
 
 /* Device-resident form: d_records (n * 168 bytes) and d_bits
  * (>= ceil(n/64)*2 words) live in HBM of the context's device `dev`; work is
- * enqueued on `hip_stream` (NULL = default stream) and NOT synchronised.
+ * enqueued on `hip_stream` and NOT synchronised. In every *_device entry point
+ * NULL means the null (default) stream, which is ordered against the
+ * blocking streams of the process, e.g. PyTorch's default stream.
  * Used by one-process-per-GPU sharding (bench.py) and by zero-copy callers. */
 int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, uint32_t mode,
                       uint32_t* d_bits, void* hip_stream);

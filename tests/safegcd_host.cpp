@@ -1,0 +1,23 @@
+// Host build of haskoin-node_amd/csrc/hkv_safegcd.h for tests/test_safegcd.py:
+// reads 64-hex-digit scalars (one per line) and prints their inverses mod n.
+#include <cstdio>
+#include <cstring>
+
+#include "../haskoin-node_amd/csrc/hkv_safegcd.h"
+
+int main() {
+  char line[128];
+  while (std::fgets(line, sizeof line, stdin)) {
+    if (std::strlen(line) < 64) continue;
+    uint32_t a[8], r[8];
+    for (int w = 0; w < 8; ++w) {
+      unsigned x = 0;
+      std::sscanf(line + 8 * (7 - w), "%8x", &x);
+      a[w] = x;
+    }
+    hkv::sgcd::inv_mod_n(r, a);
+    for (int w = 7; w >= 0; --w) std::printf("%08x", r[w]);
+    std::printf("\n");
+  }
+  return 0;
+}

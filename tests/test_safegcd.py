@@ -1,0 +1,47 @@
+"""Host build of the device safegcd scalar inversion (hkv_safegcd.h, used by
+hkv_inv_kernel for s^-1 mod n) against Python's pow(x, -1, n): the same
+source the kernel compiles, checked on edge and random scalars."""
+import os
+import random
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+@pytest.fixture(scope="module")
+def binary(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("sgcd") / "safegcd_host")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-Wno-unknown-pragmas", "-o", out,
+                    os.path.join(ROOT, "tests", "safegcd_host.cpp")], check=True)
+    return out
+
+
+def run(binary, xs):
+    inp = "".join(f"{x:064x}\n" for x in xs)
+    out = subprocess.run([binary], input=inp, capture_output=True, text=True, check=True).stdout.split()
+    return [int(h, 16) for h in out]
+
+
+def test_safegcd_edge_scalars(binary):
+    lam = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+    xs = [1, 2, 3, N - 1, N - 2, (N - 1) // 2, (N + 1) // 2, 2**255, 2**128 - 1, 2**128, 2**128 + 1,
+          2**32 - 1, 2**30, 2**30 - 1, 2**60 + 1, lam, N - lam, 0x10364141, 2**256 - 2**224 - 1 - N]
+    xs = [x % N for x in xs if x % N]
+    for x, r in zip(xs, run(binary, xs)):
+        assert r == pow(x, -1, N), hex(x)
+
+
+def test_safegcd_random(binary):
+    rng = random.Random(0x5AFE)
+    xs = [rng.randrange(1, N) for _ in range(20000)]
+    xs += [rng.getrandbits(rng.randrange(1, 256)) or 1 for _ in range(5000)]   # short scalars
+    xs += [N - (rng.getrandbits(rng.randrange(1, 128)) or 1) for _ in range(5000)]  # close to n
+    for x, r in zip(xs, run(binary, xs)):
+        assert r == pow(x, -1, N), hex(x)
+
+
+def test_safegcd_zero_maps_to_zero(binary):
+    assert run(binary, [0]) == [0]
