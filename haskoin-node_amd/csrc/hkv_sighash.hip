@@ -11,7 +11,7 @@
 //      txSigHashForkId (BIP143) -> 32-byte msg32, written with a caller
 //      stride (stride 168 writes straight into verify records).
 //   3. hkv_std_input_kernel  — per input: the non-ECDSA half of
-//      verifyStdInput for P2PK / P2PKH / P2WPKH prevouts (template match,
+//      verifyStdInput for P2PK / P2PKH / P2WPKH / P2SH-P2WPKH prevouts (template match,
 //      strict DER decode + low S + hashtype, HASH160 check, sighash) -> one
 //      168-byte verify record; a failed check writes an all-zero record, which
 //      the verify kernels reject (pubkey length 0).
@@ -794,11 +794,12 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   const bool in_range = jx < n;
   bool ok = false;
-  uint32_t kind = 0;  // 1 P2PK, 2 P2PKH, 3 P2WPKH
+  uint32_t kind = 0;  // 1 P2PK, 2 P2PKH, 3 P2WPKH, 4 P2SH-P2WPKH
   const uint32_t* row = txt;
   const uint8_t* spk = scripts;
   uint32_t sig_off = 0, sig_len = 0, pub_off = 0, pub_len = 0, sh = 0, input = 0;
   const uint8_t* pub = txs;
+  const uint8_t* prog = scripts;  // the 20-byte witness program (kinds 3, 4)
   uint64_t value = 0;
   uint32_t r[8], s[8];
 #pragma unroll
@@ -822,6 +823,8 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
         kind = 2;
       else if (L == 22 && spk[0] == 0x00u && spk[1] == 0x14u)
         kind = 3;
+      else if (L == 23 && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u)
+        kind = 4;
       ok = kind != 0;
     }
     if (ok) {
@@ -837,8 +840,18 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
         ok = read_push(txs, c, ss_end, sig_off, sig_len) && read_push(txs, c, ss_end, pub_off, pub_len) &&
              c == ss_end;
         pub = txs + pub_off;
-      } else {  // empty scriptSig, witness = [sig, pubkey]
-        ok = ss_len == 0 && (row[TXT_FLAGS] & TXF_WITNESS);
+      } else {  // witness = [sig, pubkey]; P2WPKH: empty scriptSig,
+                // P2SH-P2WPKH: scriptSig = one push of the redeem script 00 14 <h20>
+        if (kind == 3) {
+          ok = ss_len == 0;
+          prog = spk + 2;
+        } else {
+          uint32_t rd_off = 0, rd_len = 0;
+          ok = read_push(txs, c, ss_end, rd_off, rd_len) && c == ss_end && rd_len == 22u && txs[rd_off] == 0u &&
+               txs[rd_off + 1] == 0x14u;
+          prog = txs + rd_off + 2;
+        }
+        ok = ok && (row[TXT_FLAGS] & TXF_WITNESS);
         if (ok) {
           uint32_t w = walk_witness(txs, row[TXT_OUTS_END], jb.input);
           ok = get_varint(txs, w) == 2u;
@@ -880,7 +893,25 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
     uint32_t rip[5];
     ripemd160_of_digest(rip, h);
     if (need_h160) {
-      const uint8_t* hp20 = spk + (kind == 2 ? 3 : 2);
+      const uint8_t* hp20 = kind == 2 ? spk + 3 : (kind == 1 ? spk : prog);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t want = hp20[4 * k] | (hp20[4 * k + 1] << 8) | (hp20[4 * k + 2] << 16) |
+                              ((uint32_t)hp20[4 * k + 3] << 24);
+        ok = ok && want == rip[k];
+      }
+    }
+  }
+  // P2SH-P2WPKH: HASH160(redeem script 00 14 <program>) == the P2SH hash
+  const bool need_rd = ok && kind == 4;
+  if (__any(need_rd)) {
+    gen_clear(g);
+    g.code = prog - 2; g.code_len = 22; g.phase = PH_RANGE;
+    sha256_stream(h, g, need_rd, buf);
+    uint32_t rip[5];
+    ripemd160_of_digest(rip, h);
+    if (need_rd) {
+      const uint8_t* hp20 = spk + 2;
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         const uint32_t want = hp20[4 * k] | (hp20[4 * k + 1] << 8) | (hp20[4 * k + 2] << 16) |
@@ -893,7 +924,7 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   // P2WPKH -> txSigHashForkId with scriptCode = 76 a9 14 <h20> 88 ac
   JobCtx c;
   c.forkid_form = false; c.one = false; c.single_hash = false;
-  if (ok) job_setup(c, txs, row, input, sh, kind == 3, forkid);
+  if (ok) job_setup(c, txs, row, input, sh, kind >= 3, forkid);
   uint8_t* rec = recs + (size_t)jx * REC_SIZE;
   uint32_t* r32 = reinterpret_cast<uint32_t*>(rec);
   const bool need_single = ok && c.single_hash;
@@ -909,7 +940,7 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   }
   const bool live = ok && !c.one;
   if (!live) gen_clear(g);
-  else if (kind == 3) gen_job(g, c, txs, row, spk + 2, 20, true, value, r32);
+  else if (kind >= 3) gen_job(g, c, txs, row, prog, 20, true, value, r32);
   else gen_job(g, c, txs, row, spk, kind == 1 ? (pub_len + 2) : 25u, false, value, r32);
   sha256_stream(h, g, live, buf);
   sha256d_finish(d, h);

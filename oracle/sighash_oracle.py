@@ -542,8 +542,8 @@ class StdInput:
 
 
 def std_input(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[int] = None) -> StdInput:
-    """The non-ECDSA half of verifyStdInput for P2PK / P2PKH / P2WPKH
-    prevouts: template match, strict signature decode, HASH160 check and
+    """The non-ECDSA half of verifyStdInput for P2PK / P2PKH / P2WPKH /
+    P2SH-P2WPKH prevouts: template match, strict signature decode, HASH160 check and
     sighash. The input verifies iff ok and verifyHashSig(msg32, (r, s), pubkey).
     P2PK is matched in its direct-push forms (21 <33> ac, 41 <65> ac)."""
     if i >= len(tx.inputs):
@@ -581,6 +581,25 @@ def std_input(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[i
             return StdInput(False)
         r, s, sh = ts
         m = sighash_forkid(tx, p2pkh_script(prev_script[2:22]), value, i, sh, forkid)
+        return StdInput(True, m, r, s, pub)
+    if len(prev_script) == 23 and prev_script[:2] == b"\xa9\x14" and prev_script[22] == 0x87:
+        # P2SH-P2WPKH (BIP16 + BIP141): scriptSig is one push of the redeem
+        # script 00 14 <h20> whose HASH160 is the P2SH hash; then as P2WPKH.
+        # haskoin: the nested-output branch of verifyStdInput. Parity unpinned
+        # by reference data (the fixtures hold no P2SH spend).
+        items = _push_items(tx.inputs[i].script)
+        wit = tx.witness[i] if i < len(tx.witness) else []
+        if items is None or len(items) != 1 or len(wit) != 2:
+            return StdInput(False)
+        rd = items[0]
+        if len(rd) != 22 or rd[:2] != b"\x00\x14" or hash160(rd) != prev_script[2:22]:
+            return StdInput(False)
+        sig, pub = wit
+        ts = decode_tx_sig(sig, forkid)
+        if ts is None or not pubkey_bytes_ok(pub) or hash160(pub) != rd[2:22]:
+            return StdInput(False)
+        r, s, sh = ts
+        m = sighash_forkid(tx, p2pkh_script(rd[2:22]), value, i, sh, forkid)
         return StdInput(True, m, r, s, pub)
     return StdInput(False)
 

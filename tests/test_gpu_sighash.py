@@ -153,10 +153,12 @@ def device_std_records(torch, ver, raw_txs, inputs, forkid):
 def mutate_block(rng, txs, jobs, forkid):
     """Adversarial copies of signed inputs (one mutation each)."""
     out_txs, out_jobs, kinds = [], [], []
-    for m in range(14):
-        for (t, i, prev, val) in rng.sample(jobs, 6):
+    p2sh_jobs = [j for j in jobs if len(j[2]) == 23]
+    for m in range(17):
+        pool = p2sh_jobs if m >= 14 else jobs
+        for (t, i, prev, val) in rng.sample(pool, min(6, len(pool))):
             tx = sh.tx_parse(sh.tx_serialize(txs[t]))
-            seg = len(prev) == 22
+            seg = len(prev) in (22, 23)
             sig = tx.witness[i][0] if seg else sh._push_items(tx.inputs[i].script)[0]
             pub = tx.witness[i][1] if seg else (sh._push_items(tx.inputs[i].script) + [b""])[1]
             r, s = sh.sig_parse_der(sig[:-1])
@@ -188,6 +190,12 @@ def mutate_block(rng, txs, jobs, forkid):
                 sig = sh.der_encode(o.N + 5, s) + sig[-1:]               # r >= n -> 0 -> reject
             if seg:
                 tx.witness[i] = [sig, pub] if m != 13 else [sig, pub, b""]   # 13: 3 witness items
+                if m == 14:                                                   # P2SH: two pushes
+                    tx.inputs[i].script = tx.inputs[i].script * 2
+                elif m == 15:                                                 # P2SH: other program
+                    tx.inputs[i].script = txgen.push(sh.p2wpkh_script(rng.randbytes(20)))
+                elif m == 16:                                                 # P2SH: empty scriptSig
+                    tx.inputs[i].script = b""
             else:
                 tx.inputs[i].script = txgen.push(sig) + (txgen.push(pub) if pub else b"") + \
                     (b"\x51" if m == 13 else b"")                        # 13: trailing OP_1
@@ -202,7 +210,7 @@ def test_std_inputs_records_and_verdicts_vs_oracle(torch, ver, coracle, forkid):
     import hkv
     rng = random.Random(31 + (forkid or 0))
     keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 5 != 0)) for k in range(16)]
-    txs, jobs = txgen.std_block(rng, 60, keys, forkid=forkid, p2wpkh_share=0.5, p2pk_share=0.2)
+    txs, jobs = txgen.std_block(rng, 60, keys, forkid=forkid, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
     raw = [sh.tx_serialize(t) for t in txs]
     mtx, mjobs, kinds = mutate_block(rng, txs, jobs, forkid)
     all_raw = raw + mtx

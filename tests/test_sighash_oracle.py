@@ -152,10 +152,40 @@ def test_legacy_corner_cases():
 def test_std_block_generator_is_valid():
     rng = random.Random(11)
     keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(8)]
-    txs, jobs = txgen.std_block(rng, 6, keys, p2pk_share=0.2)
+    txs, jobs = txgen.std_block(rng, 10, keys, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
+    assert any(len(p) == 23 for _, _, p, _ in jobs)  # P2SH-P2WPKH present
     for t, i, prev, val in jobs:
         tx = sh.tx_parse(sh.tx_serialize(txs[t]))
         si = sh.std_input(tx, i, prev, val)
         assert si.ok
         assert o.verify_hash_sig(si.msg32, si.r, si.s, o.pubkey_parse(si.pubkey))
         assert len(sh.std_input_record(tx, i, prev, val)) == 168
+
+
+def test_p2sh_p2wpkh_rules():
+    """P2SH-P2WPKH (BIP16 + BIP141): one push of the 00 14 <h20> redeem script
+    hashing to the P2SH hash, witness [sig, pubkey], BIP143 sighash over the
+    P2PKH scriptCode of the program; every deviation rejects."""
+    rng = random.Random(12)
+    keys = [txgen.Key(rng.randrange(1, o.N)) for _ in range(4)]
+    txs, jobs = txgen.std_block(rng, 12, keys, p2wpkh_share=0.0, p2pk_share=0.0, p2sh_share=1.0)
+    t, i, prev, val = jobs[0]
+    tx = sh.tx_parse(sh.tx_serialize(txs[t]))
+    good = sh.std_input(tx, i, prev, val)
+    assert good.ok and o.verify_hash_sig(good.msg32, good.r, good.s, o.pubkey_parse(good.pubkey))
+    rd = sh._push_items(tx.inputs[i].script)[0]
+    # the same spend seen as native P2WPKH of the program signs the same message
+    tx2 = sh.tx_parse(sh.tx_serialize(tx))
+    tx2.inputs[i].script = b""
+    assert sh.std_input(tx2, i, sh.p2wpkh_script(rd[2:]), val).msg32 == good.msg32
+    for script in (b"", tx.inputs[i].script * 2, txgen.push(rd + b"\x00"), txgen.push(b"\x00\x14" + bytes(20)),
+                   b"\x51" + tx.inputs[i].script):
+        bad = sh.tx_parse(sh.tx_serialize(tx))
+        bad.inputs[i].script = script
+        assert not sh.std_input(bad, i, prev, val).ok
+    # a non-minimal push of the redeem script is still one data push
+    nm = sh.tx_parse(sh.tx_serialize(tx))
+    nm.inputs[i].script = b"\x4c\x16" + rd
+    assert sh.std_input(nm, i, prev, val).ok
+    assert not sh.std_input(tx, i, prev[:-1] + b"\x88", val).ok
+

@@ -82,9 +82,9 @@ def push(data: bytes) -> bytes:
 
 
 def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[int] = None,
-              p2wpkh_share: float = 0.6, p2pk_share: float = 0.0):
+              p2wpkh_share: float = 0.6, p2pk_share: float = 0.0, p2sh_share: float = 0.0):
     """A synthetic block mix: every tx spends 1-3 standard prevouts (P2WPKH /
-    P2PKH / P2PK) and pays 2 outputs, SIGHASH_ALL (| FORKID on a fork-id
+    P2PKH / P2PK / P2SH-P2WPKH) and pays 2 outputs, SIGHASH_ALL (| FORKID on a fork-id
     network). Returns (txs, jobs) with jobs = [(tx index, input, prevout
     script, value)]."""
     txs, jobs = [], []
@@ -95,7 +95,8 @@ def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[i
         ins = []
         for _ in range(nin):
             u = rng.random()
-            kind = "p2wpkh" if u < p2wpkh_share else ("p2pk" if u < p2wpkh_share + p2pk_share else "p2pkh")
+            kind = "p2wpkh" if u < p2wpkh_share else ("p2pk" if u < p2wpkh_share + p2pk_share else (
+                "p2sh" if u < p2wpkh_share + p2pk_share + p2sh_share else "p2pkh"))
             kinds.append(kind)
             ks.append(rng.choice(keys))
             vals.append(rng.randrange(1, 2**50))
@@ -109,11 +110,13 @@ def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[i
                 prevs.append(sh.p2wpkh_script(k.h160))
             elif kinds[j] == "p2pk":
                 prevs.append(push(k.pub) + b"\xac")
+            elif kinds[j] == "p2sh":
+                prevs.append(b"\xa9\x14" + sh.hash160(sh.p2wpkh_script(k.h160)) + b"\x87")
             else:
                 prevs.append(sh.p2pkh_script(k.h160))
         for j in range(nin):
             k = ks[j]
-            if kinds[j] == "p2wpkh":
+            if kinds[j] in ("p2wpkh", "p2sh"):
                 m = sh.sighash_forkid(tx, sh.p2pkh_script(k.h160), vals[j], j, shbyte, forkid)
             else:
                 m = sh.sighash_legacy(tx, prevs[j], vals[j], j, shbyte, forkid)
@@ -121,6 +124,9 @@ def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[i
             sig = sh.der_encode(r, s) + bytes([shbyte])
             if kinds[j] == "p2wpkh":
                 tx.witness[j] = [sig, k.pub]
+            elif kinds[j] == "p2sh":
+                tx.witness[j] = [sig, k.pub]
+                tx.inputs[j].script = push(sh.p2wpkh_script(k.h160))
             elif kinds[j] == "p2pk":
                 tx.inputs[j].script = push(sig)
             else:
