@@ -28,7 +28,7 @@ namespace hkv {
 hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im,
                            hipStream_t st);
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, hipStream_t st);
+                         uint32_t grid, uint32_t* bits, bool split, hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
 hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,

@@ -272,20 +272,33 @@ HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32
   a.v[4] = v1.x; a.v[5] = v1.y; a.v[6] = v1.z; a.v[7] = v1.w;
 }
 
+// SPLIT (small batches, when one lane per signature would leave the GPU
+// half empty): a workgroup takes 128 signatures; waves 0-1 run the k1*Q and
+// u1_lo*G half of the sum, waves 2-3 the k2*(lambda Q) and u1_hi*(2^128 G)
+// half, each with its own doubling chain (the slot loops become wave-
+// uniform, so each wave issues half the additions), and the halves meet in
+// LDS for one Jacobian addition before the x compare. The per-signature
+// dependency chain shrinks by about a quarter; total work grows by the
+// duplicated doublings and table, so large batches use SPLIT = false.
+template <bool SPLIT>
 __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits) {
-  // per wave: two G-entry slots, each 4 quads x 64 lanes x 16 B (LDS-DMA target)
+  // per wave: two G-entry slots, each 4 quads x 64 lanes x 16 B (LDS-DMA target);
+  // in SPLIT mode reused after the window loop for the half-sum exchange
   __shared__ __attribute__((aligned(16))) uint4 gpf[WG / 64][2][4][64];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ln = threadIdx.x & 63;
+  constexpr uint32_t PER_WG = SPLIT ? WG / 2 : WG;
+  const int half = SPLIT ? (wv >> 1) : 0;  // wave-uniform
+  const uint32_t sub = SPLIT ? (threadIdx.x & (PER_WG - 1)) : threadIdx.x;
 
   const uint32_t n_lanes = gridDim.x * WG;
   const uint32_t lane = blockIdx.x * WG + threadIdx.x;
 
-  for (uint32_t base = blockIdx.x * WG; base < n_pad; base += gridDim.x * WG) {
-    const uint32_t i = base + threadIdx.x;
+  for (uint32_t base = blockIdx.x * PER_WG; base < n_pad; base += gridDim.x * PER_WG) {
+    const uint32_t i = base + sub;
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
     ge q;
@@ -397,6 +410,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
 #pragma unroll 1
       for (int slot = 0; slot < 2; ++slot) {
+        if (SPLIT && slot != half) continue;
         const int dg = slot == 0 ? d1 : d2;
         const bool take = dg != 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
@@ -415,6 +429,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       if (gwin) {
 #pragma unroll 1
         for (int slot = 0; slot < 2; ++slot) {
+          if (SPLIT && slot != half) continue;
           const uint32_t gd = slot == 0 ? gd0 : gd1;
           const bool take = (gd & 0xFFFFu) != 0;
           fe tx, ty;
@@ -446,6 +461,51 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       dw = dw_next;
     }
 
+    if (SPLIT) {
+      // half 1 hands (X, Y, Z, inf) to half 0 through LDS: word-major [25][128]
+      uint32_t* xch = reinterpret_cast<uint32_t*>(&gpf[0][0][0][0]);
+      __syncthreads();  // every wave is past its last read of gpf
+      if (half == 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xch[k * PER_WG + sub] = acc.x.v[k];
+          xch[(8 + k) * PER_WG + sub] = acc.y.v[k];
+          xch[(16 + k) * PER_WG + sub] = acc.z.v[k];
+        }
+        xch[24 * PER_WG + sub] = inf ? 1u : 0u;
+      }
+      __syncthreads();
+      if (half == 0) {
+        gej b;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          b.x.v[k] = xch[k * PER_WG + sub];
+          b.y.v[k] = xch[(8 + k) * PER_WG + sub];
+          b.z.v[k] = xch[(16 + k) * PER_WG + sub];
+        }
+        const bool binf = xch[24 * PER_WG + sub] != 0;
+        // acc + b, both Jacobian on the same isomorphic curve: rescale acc by
+        // b.z (same point), then b enters as (X2, Y2) against scale Z1
+        gej a2;
+        fe z2, z3;
+        fe_sqr(z2, b.z);
+        fe_mul(z3, z2, b.z);
+        fe_mul(a2.x, acc.x, z2);
+        fe_mul(a2.y, acc.y, z3);
+        fe_mul(a2.z, acc.z, b.z);
+        bool ainf = inf;
+        gej_accumulate(a2, ainf, acc.z, b.x, b.y, !binf && !inf);
+        // acc = inf: the sum is b; b = inf: the sum is acc
+        const bool take_b = inf && !binf;
+        const bool keep_a = binf;
+        gej_cmov(a2, b, take_b);
+        gej_cmov(a2, acc, keep_a);
+        acc = a2;
+        inf = keep_a ? inf : (take_b ? false : ainf);
+      }
+      __syncthreads();  // the next window loop's G DMA reuses gpf
+    }
+
     // ---- inversion-free x compare ----
     bool accept = false;
     {
@@ -473,8 +533,8 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       accept = valid && !inf && eq;
     }
     const uint64_t ball = __ballot(accept);
-    if ((threadIdx.x & 63) == 0) {
-      const uint32_t wbase = base + (threadIdx.x & ~63u);
+    if ((threadIdx.x & 63) == 0 && half == 0) {
+      const uint32_t wbase = base + (sub & ~63u);
       if (wbase < n_pad) {
         bits[wbase / 32] = (uint32_t)ball;
         bits[wbase / 32 + 1] = (uint32_t)(ball >> 32);
@@ -794,8 +854,11 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   return hipGetLastError();
 }
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_ecmult_kernel, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits);
+                         uint32_t grid, uint32_t* bits, bool split, hipStream_t st) {
+  if (split)
+    hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits);
+  else
+    hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits);
   return hipGetLastError();
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
@@ -828,7 +891,7 @@ hipError_t launch_gen_sign(uint64_t seed, uint32_t n, const uint8_t* priv, const
   return hipGetLastError();
 }
 hipError_t ecmult_max_blocks_per_cu(int* out) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel, WG, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel<false>, WG, 0);
 }
 
 }  // namespace hkv

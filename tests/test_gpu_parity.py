@@ -317,3 +317,24 @@ def test_config5_ibd_16m_sharded_bitmap(torch, ver):
     assert (full == whole).all()
     got = adversarial.unpack_bits(full, n)
     assert (got == lab).all(), np.nonzero(got != lab)[0][:10]
+
+
+def test_split_lane_ecmult_matches_full_grid(torch, ver, coracle):
+    """Small batches run two lanes per signature (hkv_ecmult_kernel<true>,
+    chosen when the padded batch fills at most an eighth of the resident
+    grid, 32,768 signatures on an MI355X);
+    large ones one lane (<false>). The same adversarial records verified in
+    both launch shapes give identical verdicts, equal to the C oracle on a
+    slice, in both modes."""
+    from hkv import adversarial
+    n_small, n_big = 1 << 15, (1 << 15) + 257          # n_pad 32,768 (split) / 33,024 (full)
+    d = gen_device(torch, ver, n_big, seed=0x53504C54)
+    adv, lab_lib, lab_hask, _ = adversarial.mutate(d.cpu().numpy(), seed=0x53504C54)
+    d.copy_(torch.from_numpy(adv))
+    for mode, lab in ((0, lab_lib), (1, lab_hask)):
+        small = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n_small, mode), n_small)
+        big = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n_big, mode), n_big)
+        assert (small == big[:n_small]).all()
+        assert (big == lab).all() and (small == lab[:n_small]).all()
+        exp = oracle_batch(coracle, adv[: 8192 * 168].tobytes(), mode, threads=16)
+        assert (small[:8192] == exp).all()
