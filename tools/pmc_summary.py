@@ -20,6 +20,14 @@ import sys
 from collections import defaultdict
 
 
+def kname(raw: str) -> str:
+    """hkv::hkv_ecmult_kernel<false>(...) -> hkv_ecmult_kernel; <true> -> _split."""
+    k = raw.split("(")[0].replace("hkv::", "")
+    if k.startswith("void "):
+        k = k[5:]
+    return k.replace("<false>", "").replace("<true>", "_split")
+
+
 def main(src: str, dst: str) -> None:
     os.makedirs(dst, exist_ok=True)
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
@@ -32,7 +40,7 @@ def main(src: str, dst: str) -> None:
     if traces:
         durs = defaultdict(list)
         for r in csv.DictReader(open(traces[0])):
-            k = r["Kernel_Name"].split("(")[0].replace("hkv::", "")
+            k = kname(r["Kernel_Name"])
             g = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
             durs[(k, g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
         ks = {}
@@ -47,7 +55,7 @@ def main(src: str, dst: str) -> None:
     for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             g = int(r["Grid_Size"])
-            k = r["Kernel_Name"].split("(")[0].replace("hkv::", "")
+            k = kname(r["Kernel_Name"])
             if g < 65536 or not k.startswith("hkv_"):
                 continue
             per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
