@@ -472,7 +472,6 @@ HKV_DEV uint32_t walk_witness(const uint8_t* T, uint32_t wstart, uint32_t i) {
 __global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restrict__ txs,
                                                           const uint32_t* __restrict__ tx_off, uint32_t n_tx,
                                                           uint32_t want_bip143, uint32_t* __restrict__ txt) {
-  __shared__ uint32_t buf[16 * WG];
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
   const bool live = t < n_tx;
   uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -526,36 +525,35 @@ __global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restr
 #pragma unroll
     for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + k] = row[k];
   }
-  if (!want_bip143) return;
-  const bool go = live && ok;
+  (void)want_bip143;  // the BIP143 hashes: hkv_tx_hash_kernel
+}
+
+// 1b. the three BIP143 per-tx hashes, one lane per (tx, hash): blockIdx.y
+// selects hashPrevouts / hashSequence / hashOutputs (wave-uniform), so the
+// three SHA-256d streams of a tx run side by side instead of one after the
+// other (a block's index is latency-bound: one wave per 64 txs).
+__global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
+                                                         uint32_t* __restrict__ txt) {
+  __shared__ uint32_t buf[16 * WG];
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  const uint32_t which = blockIdx.y;  // 0 prevouts, 1 sequences, 2 outputs
+  const uint32_t* row = txt + (size_t)(t < n_tx ? t : 0) * TXT_WORDS;
+  const bool go = t < n_tx && (row[TXT_FLAGS] & TXF_OK);
   Gen g;
   uint32_t h[8], d[8];
-  // hashPrevouts
   gen_clear(g);
-  g.T = txs; g.nin = row[TXT_NIN]; g.ioff = row[TXT_INS]; g.j = 0; g.phase = PH_P_IN;
-  sha256_stream(h, g, go, buf);
-  sha256d_finish(d, h);
-  if (go) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + TXT_HP + k] = d[k];
+  g.T = txs;
+  if (which == 2) {  // hashOutputs (each output re-serialised canonically)
+    g.ooff = row[TXT_OUTS_FIRST]; g.ocnt = row[TXT_NOUT]; g.ret = PH_DONE; g.phase = PH_O_VAL;
+  } else {
+    g.nin = row[TXT_NIN]; g.ioff = row[TXT_INS]; g.j = 0; g.phase = which == 0 ? PH_P_IN : PH_S_IN;
   }
-  // hashSequence
-  gen_clear(g);
-  g.T = txs; g.nin = row[TXT_NIN]; g.ioff = row[TXT_INS]; g.j = 0; g.phase = PH_S_IN;
   sha256_stream(h, g, go, buf);
   sha256d_finish(d, h);
   if (go) {
+    const int slot = which == 0 ? TXT_HP : (which == 1 ? TXT_HS : TXT_HO);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + TXT_HS + k] = d[k];
-  }
-  // hashOutputs (each output re-serialised canonically)
-  gen_clear(g);
-  g.T = txs; g.ooff = row[TXT_OUTS_FIRST]; g.ocnt = row[TXT_NOUT]; g.ret = PH_DONE; g.phase = PH_O_VAL;
-  sha256_stream(h, g, go, buf);
-  sha256d_finish(d, h);
-  if (go) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + TXT_HO + k] = d[k];
+    for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + slot + k] = d[k];
   }
 }
 
@@ -981,6 +979,9 @@ hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t 
   if (n_tx == 0) return hipSuccess;
   hipLaunchKernelGGL(hkv_tx_index_kernel, dim3(blocks_for(n_tx)), dim3(WG), 0, st, txs, tx_off, n_tx, want_bip143,
                      txt);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !want_bip143) return e;
+  hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3(blocks_for(n_tx), 3), dim3(WG), 0, st, txs, n_tx, txt);
   return hipGetLastError();
 }
 hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
