@@ -109,6 +109,35 @@ def block_mix(v, torch, sptr, steps: int) -> dict:
     return out
 
 
+def host_path(v, recs, n: int, steps: int) -> dict:
+    """The drop-in boundary as the Haskell binding uses it: records in the
+    pinned host batch (hkv_batch_alloc), hkv_verify = H2D (pipelined with the
+    verify in grid-sized chunks) + kernels + D2H of the verdict words. This is
+    the PCIe-inclusive rate; `value` stays the HBM-resident one."""
+    import numpy as np
+    b = ctypes.c_void_p()
+    rc = v.lib.hkv_batch_alloc(v.ctx, n, ctypes.byref(b))
+    if rc != 0:
+        return {"error": rc}
+    try:
+        host = recs[: n * 168].cpu().numpy()
+        dst = v.lib.hkv_batch_records(b)
+        ctypes.memmove(dst, host.ctypes.data, n * 168)
+        words = np.zeros((n + 31) // 32, dtype=np.uint32)
+        wp = words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        v.lib.hkv_verify(v.ctx, b, n, 0, wp)
+        k = max(3, steps // 2)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            v.lib.hkv_verify(v.ctx, b, n, 0, wp)
+        dt = (time.perf_counter() - t0) / k
+        acc = int(np.unpackbits(words.view(np.uint8), bitorder="little")[:n].sum())
+        return {"records": n, "ms": round(dt * 1e3, 3), "verifies_per_s": round(n / dt, 1), "mismatches": n - acc,
+                "h2d_bytes": n * 168, "note": "pinned host batch -> hkv_verify (blocking), PCIe-inclusive"}
+    finally:
+        v.lib.hkv_batch_free(b)
+
+
 def header_batches(v, torch, steps: int) -> dict:
     """importHeaders' per-header work (headerHash +
     isValidPOW + linkage) for a 2,000-header peer message (a chained bchRegTest
@@ -199,6 +228,7 @@ def main() -> None:
     ap.add_argument("--no-block-mix", action="store_true")
     ap.add_argument("--no-adversarial", action="store_true")
     ap.add_argument("--no-headers", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -292,6 +322,9 @@ def main() -> None:
         mix = None
         if world == 1 and not args.no_block_mix:
             mix = block_mix(v, torch, sptr, args.steps)
+        hp = None
+        if world == 1 and not args.no_host_path:
+            hp = host_path(v, recs, n, args.steps)
         hdr = None
         if world == 1 and not args.no_headers:
             hdr = header_batches(v, torch, args.steps)
@@ -332,6 +365,7 @@ def main() -> None:
             "block_mix": mix,
             "adversarial": adv,
             "headers": hdr,
+            "host_path": hp,
         }
         print(json.dumps(line), flush=True)
     v.close()

@@ -27,6 +27,7 @@ struct DevCtx {
   int device = -1;
   int n_cu = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // H2D of host batches, overlapped with verify
   uint32_t* gtab = nullptr;
   uint32_t* qs = nullptr;
   uint32_t grid_max = 0;  // ecmult blocks (qs is sized for grid_max * WG lanes)
@@ -137,6 +138,7 @@ int init_device(DevCtx& d, int device) {
   }
   d.n_cu = prop.multiProcessorCount;
   HKV_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
+  HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
   HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 4 MiB
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
@@ -171,6 +173,7 @@ void free_device(DevCtx& d) {
     if (p) (void)hipFree(p);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.stream) (void)hipStreamDestroy(d.stream);
+  if (d.copy_stream) (void)hipStreamDestroy(d.copy_stream);
   d = DevCtx();
 }
 
@@ -367,6 +370,14 @@ static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_
     size_t lo = std::min(n, k * per), hi = std::min(n, lo + per);
     shards.push_back({lo, hi});
   }
+  std::vector<std::vector<hipEvent_t>> h2d_events(nd);
+  struct EventGuard {  // destroyed after the join below (or on an early error return)
+    std::vector<std::vector<hipEvent_t>>& e;
+    ~EventGuard() {
+      for (auto& v : e)
+        for (auto ev : v) (void)hipEventDestroy(ev);
+    }
+  } guard{h2d_events};
   for (size_t k = 0; k < nd; ++k) {
     DevCtx& d = ctx->devs[k];
     const size_t len = shards[k].hi - shards[k].lo;
@@ -388,12 +399,40 @@ static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_
               "hipHostMalloc(bits)");
       d.hbits_cap = words;
     }
-    HKV_TRY(hipMemcpyAsync(d.recs, host + shards[k].lo * hkv::REC_SIZE, len * hkv::REC_SIZE,
-                           hipMemcpyHostToDevice, d.stream),
-            "H2D records");
-    int rc = enqueue_verify(d, d.recs, len, mode, d.stream);
-    if (rc) return rc;
-    HKV_TRY(hipMemcpyAsync(d.hbits, d.bits, words * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
+    // Pipelined over chunks of whole resident grids: the copy stream moves
+    // chunk c+1 over PCIe while the verify stream works on chunk c (events
+    // order each verify after its own H2D); each chunk's verdict words go to
+    // the pinned staging right after its verify, before d.bits is reused.
+    const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
+#ifndef HKV_PIPELINE_H2D
+#define HKV_PIPELINE_H2D 1  // 0: one H2D then one verify (A/B measurement build)
+#endif
+    const size_t chunk = (HKV_PIPELINE_H2D && len >= 2 * grid_lanes)
+                             ? grid_lanes * std::max<size_t>(1, (len / 4) / grid_lanes)
+                             : len;
+    const uint8_t* src = host + shards[k].lo * hkv::REC_SIZE;
+    std::vector<hipEvent_t>& evs = h2d_events[k];
+    int rc = HKV_OK;
+    for (size_t off = 0; off < len && !rc; off += chunk) {
+      const size_t cl = std::min(chunk, len - off);
+      hipEvent_t ev = nullptr;
+      HKV_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+      evs.push_back(ev);
+      HKV_TRY(hipMemcpyAsync(d.recs + off * hkv::REC_SIZE, src + off * hkv::REC_SIZE, cl * hkv::REC_SIZE,
+                             hipMemcpyHostToDevice, d.copy_stream),
+              "H2D records");
+      HKV_TRY(hipEventRecord(ev, d.copy_stream), "hipEventRecord");
+      HKV_TRY(hipStreamWaitEvent(d.stream, ev, 0), "hipStreamWaitEvent");
+      rc = enqueue_verify(d, d.recs + off * hkv::REC_SIZE, cl, mode, d.stream);
+      if (!rc)
+        HKV_TRY(hipMemcpyAsync(d.hbits + off / 32, d.bits, (cl + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream),
+                "D2H bits");
+    }
+    if (rc) {
+      (void)hipStreamSynchronize(d.copy_stream);
+      (void)hipStreamSynchronize(d.stream);
+      return rc;
+    }
   }
   for (size_t k = 0; k < nd; ++k) {
     DevCtx& d = ctx->devs[k];

@@ -338,3 +338,26 @@ def test_split_lane_ecmult_matches_full_grid(torch, ver, coracle):
         assert (big == lab).all() and (small == lab[:n_small]).all()
         exp = oracle_batch(coracle, adv[: 8192 * 168].tobytes(), mode, threads=16)
         assert (small[:8192] == exp).all()
+
+
+def test_host_path_pipelined_chunks_match_device_path(torch, ver):
+    """hkv_verify_host over 600,000 records is pipelined in grid-sized chunks
+    (H2D of chunk c+1 on the copy stream while chunk c verifies; here
+    262,144 + 262,144 + 75,712): the verdict bitmap equals the HBM-resident
+    path's, with 1% of the records corrupted so both verdicts occur."""
+    n = 600_000
+    d = gen_device(torch, ver, n, seed=0x484F5354)
+    host = d.cpu().numpy().copy()
+    rng = np.random.default_rng(9)
+    bad = rng.choice(n, size=n // 100, replace=False)
+    host[bad * 168 + 5] ^= 0x40                       # flip a msg32 bit: ECDSA rejects
+    d.copy_(torch.from_numpy(host))
+    dev = adversarial_unpack(verify_dev_bits(torch, ver, d, n, 0), n)
+    got = ver.verify_records(host, 0)
+    assert (got == dev).all()
+    assert not got[bad].any() and got.sum() == n - bad.size
+
+
+def adversarial_unpack(words, n):
+    from hkv import adversarial
+    return adversarial.unpack_bits(words, n)
