@@ -7,7 +7,7 @@
 //   2. hkv_ecmult_kernel    — per-lane table of 1..8 * Q on an isomorphic
 //      curve (one common Z, so all Q additions are mixed), then a shared
 //      doubling chain of 132 bits with radix-16 Booth digits for k1*Q and
-//      k2*(lambda Q) and radix-256 Booth digits for u1_lo*G and
+//      k2*(lambda Q) and radix-2^20 Booth digits for u1_lo*G and
 //      u1_hi*(2^128 G) (G tables staged in LDS), then the inversion-free
 //      Jacobian x compare (r*Z^2 == X, and (r+n)*Z^2 == X when r < p-n).
 //      Verdicts leave as a ballot bitmap, one 64-bit word per wave.
@@ -153,7 +153,7 @@ HKV_DEV void shr_bits(uint32_t* a, int b) {
   for (int q = 0; q < L - 1; ++q) a[q] = (a[q] >> b) | (a[q + 1] << (32 - b));
   a[L - 1] >>= b;
 }
-// Radix-16 / radix-256 Booth recoding (LSB first, MSB-first consumption in
+// Radix-16 / radix-2^20 Booth recoding (LSB first, MSB-first consumption in
 // the ecmult kernel): d = ((v + 1) >> 1) - ((v >> W) << W), v = bits
 // [pos-1, pos+W-1]; sum_w d_w 16^w reproduces the scalar (< 2^131).
 HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2,
@@ -173,15 +173,16 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
   uint32_t pl = 0, ph = 0;
 #pragma unroll 1
   for (int j = 0; j < GWIN; ++j) {
-    const uint32_t vl = pl | ((SL[0] & 0xFFFFu) << 1), vh = ph | ((SH[0] & 0xFFFFu) << 1);
-    pl = (SL[0] >> 15) & 1u;
-    ph = (SH[0] >> 15) & 1u;
-    shr_bits<4>(SL, 16);
-    shr_bits<4>(SH, 16);
-    const int dl = (int)((vl + 1u) >> 1) - (int)((vl >> 16) << 16);
-    const int dh = (int)((vh + 1u) >> 1) - (int)((vh >> 16) << 16);
-    im[(size_t)(IM_GDIG + 2 * j) * n_pad + i] = (uint32_t)(dl < 0 ? -dl : dl) | (dl < 0 ? 0x10000u : 0u);
-    im[(size_t)(IM_GDIG + 2 * j + 1) * n_pad + i] = (uint32_t)(dh < 0 ? -dh : dh) | (dh < 0 ? 0x10000u : 0u);
+    constexpr uint32_t M = (1u << GTAB_W) - 1u;
+    const uint32_t vl = pl | ((SL[0] & M) << 1), vh = ph | ((SH[0] & M) << 1);
+    pl = (SL[0] >> (GTAB_W - 1)) & 1u;
+    ph = (SH[0] >> (GTAB_W - 1)) & 1u;
+    shr_bits<4>(SL, GTAB_W);
+    shr_bits<4>(SH, GTAB_W);
+    const int dl = (int)((vl + 1u) >> 1) - (int)((vl >> GTAB_W) << GTAB_W);
+    const int dh = (int)((vh + 1u) >> 1) - (int)((vh >> GTAB_W) << GTAB_W);
+    im[(size_t)(IM_GDIG + 2 * j) * n_pad + i] = (uint32_t)(dl < 0 ? -dl : dl) | (dl < 0 ? GD_NEG : 0u);
+    im[(size_t)(IM_GDIG + 2 * j + 1) * n_pad + i] = (uint32_t)(dh < 0 ? -dh : dh) | (dh < 0 ? GD_NEG : 0u);
   }
 }
 
@@ -386,13 +387,13 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
       const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
-      const bool gwin = (win & 3) == 0;
+      const bool gwin = (win % GSTEP) == 0;
       uint32_t gd0 = 0, gd1 = 0;
       if (gwin) {
-        const int gj = win >> 2;
+        const int gj = win / GSTEP;
         gd0 = valid ? im[(size_t)(IM_GDIG + 2 * gj) * n_pad + i] : 0u;
         gd1 = valid ? im[(size_t)(IM_GDIG + 2 * gj + 1) * n_pad + i] : 0u;
-        const uint32_t m0 = gd0 & 0xFFFFu, m1 = gd1 & 0xFFFFu;
+        const uint32_t m0 = gd0 & GD_MAG, m1 = gd1 & GD_MAG;
         const uint4* e0 = reinterpret_cast<const uint4*>(gtab) + (size_t)(m0 ? m0 - 1 : 0) * 4;
         const uint4* e1 = reinterpret_cast<const uint4*>(gtab) + ((size_t)GTAB_ENTRIES + (m1 ? m1 - 1 : 0)) * 4;
 #pragma unroll
@@ -424,14 +425,14 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         gej_accumulate(acc, inf, acc.z, tx, ty, take);
         gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
       }
-      // G terms every fourth window (radix 2^16): slot 0 = u1_lo * G,
+      // G terms every fifth window (radix 2^20): slot 0 = u1_lo * G,
       // slot 1 = u1_hi * 2^128 G; entries were DMA'd into LDS before the doublings.
       if (gwin) {
 #pragma unroll 1
         for (int slot = 0; slot < 2; ++slot) {
           if (SPLIT && slot != half) continue;
           const uint32_t gd = slot == 0 ? gd0 : gd1;
-          const bool take = (gd & 0xFFFFu) != 0;
+          const bool take = (gd & GD_MAG) != 0;
           fe tx, ty;
           {
             const uint4 a0 = gpf[wv][slot][0][ln], a1 = gpf[wv][slot][1][ln];
@@ -443,7 +444,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
           }
           fe nty;
           fe_neg(nty, ty);
-          fe_cmov(ty, nty, (gd & 0x10000u) != 0);
+          fe_cmov(ty, nty, (gd & GD_NEG) != 0);
           fe az;
           fe_mul(az, acc.z, Zg);
           const bool was_inf = inf;

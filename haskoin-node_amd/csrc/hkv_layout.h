@@ -20,18 +20,20 @@ enum : int {
   IM_R = 35,      // 8 limbs, r (< n)
   IM_C = 43,      // 8 limbs, batch-inversion prefix product, then s^-1
   IM_DIG = 51,    // 33 words: window w's radix-16 Booth digits of k1, k2
-  IM_GDIG = 84,   // 2 x 9 words: radix-2^16 Booth digits of u1_lo, u1_hi
-  IM_WORDS = 102,
+  IM_GDIG = 84,   // 2 x 7 words: radix-2^20 Booth digits of u1_lo, u1_hi
+  IM_WORDS = 98,
   // between the parse and scalar kernels: s (normalised) and m = msg mod n
   IM_S = IM_K1,   // 8 limbs over K1|K2 (10 words)
   IM_M = IM_U1L,  // 8 limbs over U1L|U1H
 };
 // Q digit word of window w (w = 0..32, bit position 4w): biased Booth digits
 //   bits 0-4 d1 + 8 (k1, radix 16, -8..8), bits 5-9 d2 + 8 (k2)
-// G digit word of G window j (j = 0..8, bit position 16j = Q window 4j),
-// one per u1 half: bits 0-15 |d| (0..32768), bit 16 sign.
+// G digit word of G window j (j = 0..6, bit position 20j = Q window 5j),
+// one per u1 half: bits 0-19 |d| (0..2^19), bit 20 sign.
 constexpr int NWIN = 33;
-constexpr int GWIN = 9;
+constexpr int GWIN = 7;
+constexpr int GSTEP = 5;                      // Q windows per G window
+constexpr uint32_t GD_MAG = 0xFFFFFu, GD_NEG = 0x100000u;
 constexpr uint32_t DIG_ZERO = 8u | (8u << 5);
 
 // signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
@@ -39,11 +41,11 @@ constexpr uint32_t DIG_ZERO = 8u | (8u << 5);
 constexpr int BATCH_INV = 16;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
-// Fixed-base tables in HBM (4 MiB, L2/MALL resident): multiples j*B for
-// j = 1..32768, B in {G, 2^128 G}, affine, 16 dwords per entry
-// [x(8) | y(8)], table t at entry offset t*32768. Gathered per lane by
-// LDS-DMA one window ahead of use.
-constexpr int GTAB_W = 16;             // Booth radix 2^16
+// Fixed-base tables in HBM (64 MiB, MALL resident): multiples j*B for
+// j = 1..2^19, B in {G, 2^128 G}, affine, 16 dwords per entry
+// [x(8) | y(8)], table t at entry offset t*2^19. Gathered per lane by
+// LDS-DMA at the start of the window that adds them (four doublings ahead).
+constexpr int GTAB_W = 20;             // Booth radix 2^20
 constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
 constexpr size_t GTAB_DWORDS = 2ull * GTAB_ENTRIES * 16;
 

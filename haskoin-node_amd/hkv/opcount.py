@@ -25,7 +25,7 @@ GEJ_ADD_GE = 8 * FE_MUL + 3 * FE_SQR                          # mixed add
 GEJ_ADD_ZINV = GEJ_ADD_GE + FE_MUL                            # + az = Z*Zg
 
 Q_WINDOWS = 33       # radix-16 Booth over 132 bits
-G_WINDOWS = 9        # radix-2^16 Booth over 144 bits (u1 halves)
+G_WINDOWS = 7        # radix-2^20 Booth over 140 bits (u1 halves)
 DOUBLINGS = 4 * (Q_WINDOWS - 1)
 
 SC_INV_LOW = 0x0BAAEDCE6AF48A03BBFD25E8CD036413F

@@ -60,7 +60,8 @@ def booth(k, w, nwin):
 
 
 def test_booth_recoding_identity():
-    """Radix-16 / radix-256 Booth digits as the ecmult kernel extracts them."""
+    """Radix-16 (Q) / radix-2^20 (G, hkv_layout.h GTAB_W) Booth digits as the
+    ecmult kernel extracts them."""
     rng = random.Random(9)
     for _ in range(2000):
         k = rng.randrange(2**131)
@@ -68,9 +69,10 @@ def test_booth_recoding_identity():
         assert all(-8 <= x <= 8 for x in d)
         assert sum(x * 16**i for i, x in enumerate(d)) == k
         u = rng.randrange(2**128)
-        e = booth(u, 8, 17)
-        assert all(-128 <= x <= 128 for x in e)
-        assert sum(x * 256**i for i, x in enumerate(e)) == u
+        e = booth(u, 20, 7)                        # GWIN = 7 windows of 20 bits
+        assert all(-2**19 <= x <= 2**19 for x in e)
+        assert sum(x * 2**(20 * i) for i, x in enumerate(e)) == u
+        assert all(abs(x) < 2**20 for x in e)       # fits GD_MAG (20 bits)
 
 
 def test_reference_fixture_hashes():
