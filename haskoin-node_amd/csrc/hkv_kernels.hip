@@ -47,7 +47,10 @@ __constant__ static const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC
 // ---------------------------------------------------------------------------
 // 1. prologue
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(WG, 4) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
+#ifndef HKV_PROLOGUE_WAVES
+#define HKV_PROLOGUE_WAVES 4  // min waves per SIMD the prologue's register allocation targets
+#endif
+__global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
                                                           uint32_t n_pad, uint32_t mode,
                                                           uint32_t* __restrict__ im) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
