@@ -20,20 +20,26 @@ enum : int {
   IM_R = 35,      // 8 limbs, r (< n)
   IM_C = 43,      // 8 limbs, batch-inversion prefix product, then s^-1
   IM_DIG = 51,    // 33 words: window w's radix-16 Booth digits of k1, k2
-  IM_GDIG = 84,   // 2 x 7 words: radix-2^20 Booth digits of u1_lo, u1_hi
-  IM_WORDS = 98,
+  IM_GDIG = 84,   // 2 x GWIN words: radix-2^GTAB_W Booth digits of u1_lo, u1_hi
   // between the parse and scalar kernels: s (normalised) and m = msg mod n
   IM_S = IM_K1,   // 8 limbs over K1|K2 (10 words)
   IM_M = IM_U1L,  // 8 limbs over U1L|U1H
 };
 // Q digit word of window w (w = 0..32, bit position 4w): biased Booth digits
 //   bits 0-4 d1 + 8 (k1, radix 16, -8..8), bits 5-9 d2 + 8 (k2)
-// G digit word of G window j (j = 0..6, bit position 20j = Q window 5j),
-// one per u1 half: bits 0-19 |d| (0..2^19), bit 20 sign.
+// G digit word of G window j (j = 0..GWIN-1, bit position GTAB_W*j = Q
+// window GSTEP*j), one per u1 half: bits 0..GTAB_W-1 |d| (0..2^(GTAB_W-1)),
+// bit GTAB_W sign. Default radix 2^20: 7 windows, every fifth Q window.
+#ifndef HKV_GTAB_W
+#define HKV_GTAB_W 20
+#endif
+constexpr int GTAB_W = HKV_GTAB_W;            // Booth radix of the fixed-base tables
+static_assert(GTAB_W % 4 == 0 && GTAB_W >= 8 && GTAB_W <= 28, "G windows sit on Q window boundaries");
 constexpr int NWIN = 33;
-constexpr int GWIN = 7;
-constexpr int GSTEP = 5;                      // Q windows per G window
-constexpr uint32_t GD_MAG = 0xFFFFFu, GD_NEG = 0x100000u;
+constexpr int GWIN = (128 + GTAB_W) / GTAB_W;  // covers 129 bits with the Booth carry
+constexpr int GSTEP = GTAB_W / 4;              // Q windows per G window
+constexpr uint32_t GD_MAG = (1u << GTAB_W) - 1u, GD_NEG = 1u << GTAB_W;
+constexpr int IM_WORDS = IM_GDIG + 2 * GWIN;
 constexpr uint32_t DIG_ZERO = 8u | (8u << 5);
 
 // signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
@@ -45,7 +51,6 @@ constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF
 // j = 1..2^19, B in {G, 2^128 G}, affine, 16 dwords per entry
 // [x(8) | y(8)], table t at entry offset t*2^19. Gathered per lane by
 // LDS-DMA at the start of the window that adds them (four doublings ahead).
-constexpr int GTAB_W = 20;             // Booth radix 2^20
 constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
 constexpr size_t GTAB_DWORDS = 2ull * GTAB_ENTRIES * 16;
 
