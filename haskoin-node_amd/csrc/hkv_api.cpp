@@ -139,7 +139,7 @@ int init_device(DevCtx& d, int device) {
   d.n_cu = prop.multiProcessorCount;
   HKV_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
   HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
-  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 4 MiB
+  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 64 MiB at radix 2^20
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
   if (per_cu < 1) per_cu = 1;
