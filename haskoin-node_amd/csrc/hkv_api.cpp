@@ -115,7 +115,10 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // dependency chain where latency, not issue, bounds the launch. Above that
   // the duplicated doublings cost more than the chain saves (measured: a
   // 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms unsplit).
-  const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / 8;
+#ifndef HKV_SPLIT_DIV
+#define HKV_SPLIT_DIV 8  // split when n_pad <= resident grid / HKV_SPLIT_DIV
+#endif
+  const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
   const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, d.bits, split, st),
