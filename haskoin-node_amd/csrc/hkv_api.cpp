@@ -46,8 +46,8 @@ struct DevCtx {
   uint32_t* txt = nullptr;
   size_t txt_cap = 0;  // bytes
   // [0..3] tx batch, [4] sighash out, [5] header batch
-  void* stage[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  size_t stage_cap[6] = {0, 0, 0, 0, 0, 0};
+  void* stage[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t stage_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -702,6 +702,54 @@ int hkv_check_headers(hkv_ctx* ctx, const uint8_t* headers, size_t n, const uint
   HKV_TRY(hipMemcpyAsync(hashes_out, dhash, n * 32, hipMemcpyDeviceToHost, d.stream), "D2H header hashes");
   HKV_TRY(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, d.stream), "D2H header status");
   HKV_TRY(hipStreamSynchronize(d.stream), "headers sync");
+  return HKV_OK;
+}
+
+int hkv_merkle_roots_device(hkv_ctx* ctx, int dev, const uint8_t* d_txids, const uint32_t* d_offsets,
+                            size_t n_blocks, uint8_t* d_scratch, uint8_t* d_roots, uint8_t* d_mutated,
+                            void* hip_stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || n_blocks > 0x7FFFFFFFull) return HKV_E_ARG;
+  if (n_blocks == 0) return HKV_OK;
+  if (!d_txids || !d_offsets || !d_scratch || !d_roots || !d_mutated || !aligned(d_txids, 16) ||
+      !aligned(d_scratch, 16) || !aligned(d_roots, 16) || !aligned(d_offsets, 4))
+    return HKV_E_ARG;
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
+  HKV_TRY(hkv::launch_merkle(d_txids, d_offsets, (uint32_t)n_blocks, d_scratch, d_roots, d_mutated, st),
+          "merkle launch");
+  return HKV_OK;
+}
+
+int hkv_merkle_roots(hkv_ctx* ctx, const uint8_t* txids, const uint32_t* offsets, size_t n_blocks,
+                     uint8_t* roots_out, uint8_t* mutated) {
+  if (!ctx || ctx->devs.empty() || n_blocks > 0x7FFFFFFFull) return HKV_E_ARG;
+  if (n_blocks == 0) return HKV_OK;
+  if (!offsets || !roots_out || !mutated) return HKV_E_ARG;
+  if (offsets[0] != 0) return HKV_E_ARG;
+  for (size_t b = 0; b < n_blocks; ++b)
+    if (offsets[b + 1] < offsets[b]) return HKV_E_ARG;
+  const size_t leaves = offsets[n_blocks];
+  if (leaves && !txids) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[0];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  // one staging buffer: txids (L*32) | scratch (L*32) | roots (B*32) | offsets ((B+1)*4) | mutated (B)
+  const size_t off_bytes = (n_blocks + 1) * 4;
+  int rc = grow(&d.stage[6], &d.stage_cap[6], leaves * 64 + n_blocks * 32 + off_bytes + n_blocks,
+                "hipMalloc(merkle batch)");
+  if (rc) return rc;
+  uint8_t* b = static_cast<uint8_t*>(d.stage[6]);
+  uint8_t *dl = b, *dsc = dl + leaves * 32, *dr = dsc + leaves * 32, *doff = dr + n_blocks * 32,
+          *dm = doff + off_bytes;
+  if (leaves) HKV_TRY(hipMemcpyAsync(dl, txids, leaves * 32, hipMemcpyHostToDevice, d.stream), "H2D txids");
+  HKV_TRY(hipMemcpyAsync(doff, offsets, off_bytes, hipMemcpyHostToDevice, d.stream), "H2D merkle offsets");
+  HKV_TRY(hkv::launch_merkle(dl, reinterpret_cast<const uint32_t*>(doff), (uint32_t)n_blocks, dsc, dr, dm,
+                             d.stream),
+          "merkle launch");
+  HKV_TRY(hipMemcpyAsync(roots_out, dr, n_blocks * 32, hipMemcpyDeviceToHost, d.stream), "D2H merkle roots");
+  HKV_TRY(hipMemcpyAsync(mutated, dm, n_blocks, hipMemcpyDeviceToHost, d.stream), "D2H merkle mutated");
+  HKV_TRY(hipStreamSynchronize(d.stream), "merkle sync");
   return HKV_OK;
 }
 

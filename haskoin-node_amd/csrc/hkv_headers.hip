@@ -133,6 +133,103 @@ __global__ void __launch_bounds__(WG) hkv_header_link_kernel(const uint32_t* __r
   if (diff == 0) status[i] = (uint8_t)(status[i] | HKV_HDR_LINK_OK);
 }
 
+// ---------------------------------------------------------------------------
+// Block merkle roots. The reference's own block test
+// asserts b.header.merkle == buildMerkleRoot (txHash <$> b.txs)
+// (/root/reference/test/Haskoin/NodeSpec.hs:185-193) on blocks fetched by
+// getBlocks (src/Haskoin/Node/Peer.hs:309-344); buildMerkleRoot is
+// haskoin-core-1.1.0 Haskoin.Block.Merkle [dep]: pairwise SHA-256d of
+// 64-byte concatenations, an odd level's last hash paired with itself.
+// `mutated` is Bitcoin Core's CVE-2012-2459 flag (two equal hashes paired
+// at any level), so a caller can reject a duplicated-tx block whose root
+// still matches.
+//
+// One workgroup per block: a 256-lane sweep per level, levels separated by
+// workgroup barriers, the tree built in place in the block's own scratch
+// range (chunk k writes [256k, 256k+256) after chunk k/2 has read it).
+// Algorithmic work: 3 SHA-256 compressions per inner node (n - 1 nodes per
+// n-leaf block), 96 B of traffic per node.
+
+// SHA-256d of a||b, both 32-byte digests held as little-endian words of the
+// digest bytes; out in the same form.
+HKV_DEV void sha256d_pair(uint32_t out[8], const uint32_t a[8], const uint32_t b[8]) {
+  uint32_t st[8], w[16];
+  sha256_init(st);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { w[k] = __builtin_bswap32(a[k]); w[8 + k] = __builtin_bswap32(b[k]); }
+  sha256_compress(st, w);
+  w[0] = 0x80000000u;
+#pragma unroll
+  for (int k = 1; k < 15; ++k) w[k] = 0;
+  w[15] = 512;
+  sha256_compress(st, w);
+  uint32_t d[8];
+  sha256_of_digest(d, st);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = __builtin_bswap32(d[k]);
+}
+
+HKV_DEV void load8(uint32_t v[8], const uint32_t* p) {
+  const uint4 x = *reinterpret_cast<const uint4*>(p), y = *reinterpret_cast<const uint4*>(p + 4);
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
+HKV_DEV void store8(uint32_t* p, const uint32_t v[8]) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<uint4*>(p + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+}
+
+__global__ void __launch_bounds__(WG) hkv_merkle_kernel(const uint32_t* __restrict__ leaves,
+                                                        const uint32_t* __restrict__ offsets,
+                                                        uint32_t* __restrict__ scratch, uint32_t* __restrict__ roots,
+                                                        uint8_t* __restrict__ mutated) {
+  const uint32_t blk = blockIdx.x;
+  const uint32_t off = offsets[blk];
+  uint32_t cnt = offsets[blk + 1] - off;
+  const uint32_t* src = leaves + (size_t)off * 8;
+  uint32_t* tree = scratch + (size_t)off * 8;
+  int mut = 0;
+  while (cnt > 1) {  // cnt is workgroup-uniform: every barrier below is reached by all lanes
+    const uint32_t half = (cnt + 1) >> 1;
+    for (uint32_t base = 0; base < half; base += WG) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t o[8];
+      if (i < half) {
+        uint32_t a[8], b[8];
+        const uint32_t j = 2 * i + 1 < cnt ? 2 * i + 1 : cnt - 1;
+        load8(a, src + (size_t)(2 * i) * 8);
+        load8(b, src + (size_t)j * 8);
+        if (j != 2 * i) {
+          uint32_t diff = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) diff |= a[k] ^ b[k];
+          mut |= diff == 0;
+        }
+        sha256d_pair(o, a, b);
+      }
+      __syncthreads();  // this chunk's reads precede its in-place writes
+      if (i < half) store8(tree + (size_t)i * 8, o);
+      __syncthreads();
+    }
+    src = tree;
+    cnt = half;
+  }
+  mut = __syncthreads_or(mut);
+  if (threadIdx.x == 0) {
+    uint32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (cnt == 1) load8(r, src);  // cnt == 0: an empty block, all-zero root
+    store8(roots + (size_t)blk * 8, r);
+    mutated[blk] = (uint8_t)(mut != 0);
+  }
+}
+
+hipError_t launch_merkle(const uint8_t* leaves, const uint32_t* offsets, uint32_t n_blocks, uint8_t* scratch,
+                         uint8_t* roots, uint8_t* mutated, hipStream_t st) {
+  if (n_blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(hkv_merkle_kernel, dim3(n_blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(leaves),
+                     offsets, reinterpret_cast<uint32_t*>(scratch), reinterpret_cast<uint32_t*>(roots), mutated);
+  return hipGetLastError();
+}
+
 hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
                           uint8_t* hashes, uint8_t* status, hipStream_t st) {
   if (n == 0) return hipSuccess;

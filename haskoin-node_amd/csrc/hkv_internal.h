@@ -51,4 +51,6 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
 // hkv_headers.hip
 hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
                           uint8_t* hashes, uint8_t* status, hipStream_t st);
+hipError_t launch_merkle(const uint8_t* leaves, const uint32_t* offsets, uint32_t n_blocks, uint8_t* scratch,
+                         uint8_t* roots, uint8_t* mutated, hipStream_t st);
 }  // namespace hkv

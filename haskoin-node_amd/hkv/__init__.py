@@ -9,6 +9,7 @@ from .lib import (HKV_HASKOIN, HKV_LIBSECP, HKV_NO_FORKID, HKV_RECORD_SIZE, HKV_
                   HKV_SIGHASH_LEGACY, HkvError, HkvTxs, lib_path, load_library)
 from .records import make_record, pack_records, unpack_bits
 from .headers import check_headers, check_headers_device
+from .merkle import merkle_roots, merkle_roots_device
 from .sighash import TxBatch, tx_sig_hash_batch, verify_std_inputs
 from .verify import (Verifier, VerifierConfig, verify_hash_sig_batch,
                      verify_raw_batch)
@@ -19,4 +20,5 @@ __all__ = [
     "VerifierConfig", "verify_hash_sig_batch", "verify_raw_batch", "HKV_NO_FORKID",
     "HKV_SIGHASH_FORKID", "HKV_SIGHASH_LEGACY", "HkvTxs", "TxBatch", "tx_sig_hash_batch",
     "verify_std_inputs", "check_headers", "check_headers_device",
+    "merkle_roots", "merkle_roots_device",
 ]

@@ -83,6 +83,9 @@ EXPORTS = {
                                              c_void_p, c_void_p, c_void_p]),
     "hkv_verify_std_inputs": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
                                       POINTER(c_uint32)]),
+    "hkv_merkle_roots": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
+    "hkv_merkle_roots_device": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
     "hkv_check_headers": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hkv_check_headers_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p]),

@@ -227,6 +227,26 @@ int hkv_check_headers(hkv_ctx* ctx, const uint8_t* headers, size_t n, const uint
 int hkv_check_headers_device(hkv_ctx* ctx, int dev, const uint8_t* d_headers, size_t n, const uint8_t* d_pow_limit,
                              const uint8_t* d_prev_hash, uint8_t* d_hashes, uint8_t* d_status, void* hip_stream);
 
+/* ---------------------------------------------------------------------------
+ * Block merkle roots: haskoin-core buildMerkleRoot [dep, haskoin-core-1.1.0
+ * Haskoin.Block.Merkle], as the reference's block test applies it
+ * (/root/reference/test/Haskoin/NodeSpec.hs:185-193: b.header.merkle ==
+ * buildMerkleRoot (txHash <$> b.txs)) to blocks from getBlocks
+ * (src/Haskoin/Node/Peer.hs:309-344). Batched over many blocks.
+ * txids: offsets[n_blocks] * 32 bytes, digest order (txHash serialisation);
+ * block b owns txids [offsets[b], offsets[b+1]). roots_out: n_blocks * 32
+ * (an empty block gets 32 zero bytes). mutated: n_blocks bytes, 1 when two
+ * equal hashes are paired at some level (CVE-2012-2459 duplicate-tx form).
+ * Host memory, first device, blocking. */
+int hkv_merkle_roots(hkv_ctx* ctx, const uint8_t* txids, const uint32_t* offsets, size_t n_blocks,
+                     uint8_t* roots_out, uint8_t* mutated);
+/* Device form: every pointer in HBM of device `dev`; d_scratch holds
+ * offsets[n_blocks] * 32 bytes and may alias nothing else; 16-byte aligned
+ * txids / scratch / roots. Enqueued on hip_stream, not synchronised. */
+int hkv_merkle_roots_device(hkv_ctx* ctx, int dev, const uint8_t* d_txids, const uint32_t* d_offsets,
+                            size_t n_blocks, uint8_t* d_scratch, uint8_t* d_roots, uint8_t* d_mutated,
+                            void* hip_stream);
+
 /* Synthetic-data hooks (block-mix generator, off the verify path):
  * n random private keys -> d_priv (n*32, big-endian), compressed public keys
  * d_pub (n*33) and their HASH160 d_h160 (n*20);
