@@ -217,6 +217,48 @@ def adversarial_mix(v, torch, recs, n: int, sptr: int, steps: int) -> dict:
     return out
 
 
+def merkle_batches(v, torch, steps: int) -> dict:
+    """Block merkle roots (buildMerkleRoot, NodeSpec.hs:185-193) on HBM-resident
+    txids: one 2,000-tx block (latency) and 4,096 blocks of 2,000 txs
+    (throughput). Work: n-1 inner nodes per n-tx block, 3 SHA-256 compressions
+    per node."""
+    import numpy as np
+    from hkv import merkle as mk
+    rng = np.random.default_rng(0x4D4B4C31)
+    out = {}
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    for label, nb, ntx in (("block2000", 1, 2000), ("batch4096", 4096, 2000)):
+        offsets = (np.arange(nb + 1, dtype=np.int64) * ntx).astype(np.int32)
+        nl = nb * ntx
+        dl = torch.from_numpy(rng.integers(0, 256, size=nl * 32, dtype=np.uint8)).cuda()
+        do = torch.from_numpy(offsets).cuda()
+        sc = torch.zeros(nl * 32, dtype=torch.uint8, device="cuda")
+        dr = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda")
+        dm = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+
+        def run():
+            mk.merkle_roots_device(v, 0, dl.data_ptr(), do.data_ptr(), nb, sc.data_ptr(), dr.data_ptr(),
+                                   dm.data_ptr(), sp)
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k = max(5, steps)
+        e0.record(stream)
+        for _ in range(k):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / k
+        nodes = nb * (ntx - 1)
+        out[label] = {"blocks": nb, "txs_per_block": ntx, "us": round(us, 1),
+                      "blocks_per_s": round(nb / (us * 1e-6), 1), "nodes_per_s": round(nodes / (us * 1e-6), 1),
+                      "mutated": int(dm.sum().item())}
+    out["workload"] = ("buildMerkleRoot per block (NodeSpec.hs:185-193 / haskoin-core Merkle [dep]), random "
+                       "txids resident in HBM, one workgroup per block")
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +270,7 @@ def main() -> None:
     ap.add_argument("--no-block-mix", action="store_true")
     ap.add_argument("--no-adversarial", action="store_true")
     ap.add_argument("--no-headers", action="store_true")
+    ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
@@ -328,6 +371,9 @@ def main() -> None:
         hdr = None
         if world == 1 and not args.no_headers:
             hdr = header_batches(v, torch, args.steps)
+        mkl = None
+        if world == 1 and not args.no_merkle:
+            mkl = merkle_batches(v, torch, args.steps)
         adv = None
         if world == 1 and not args.no_adversarial:
             adv = adversarial_mix(v, torch, recs, n, sptr, args.steps)
@@ -365,6 +411,7 @@ def main() -> None:
             "block_mix": mix,
             "adversarial": adv,
             "headers": hdr,
+            "merkle": mkl,
             "host_path": hp,
         }
         print(json.dumps(line), flush=True)
