@@ -222,9 +222,145 @@ __global__ void __launch_bounds__(WG) hkv_merkle_kernel(const uint32_t* __restri
   }
 }
 
+// Few-block batches: each block's tree is cut into MERKLE_SPLIT aligned
+// subtrees of 2^H leaves (H smallest with ceil(n / 2^H) <= MERKLE_SPLIT), one
+// workgroup each, so a lone block's lower levels run on several CUs. An
+// aligned subtree root is a node of the full tree; the rightmost one, when it
+// collapses below height H, is paired with itself up to H exactly as the full
+// tree's odd-level rule does. Subtree root -> its slot 0 in scratch, its
+// mutated flag -> word 0 of slot 1 (written only when it has >= 2 leaves).
+// hkv_merkle_top_kernel then joins the m <= MERKLE_SPLIT roots per block.
+constexpr uint32_t MERKLE_SPLIT = 8;
+
+HKV_DEV uint32_t merkle_split_height(uint32_t cnt) {
+  uint32_t h = 0;
+  while (((cnt + (1u << h) - 1) >> h) > MERKLE_SPLIT) ++h;
+  return h;
+}
+
+__global__ void __launch_bounds__(WG) hkv_merkle_sub_kernel(const uint32_t* __restrict__ leaves,
+                                                            const uint32_t* __restrict__ offsets,
+                                                            uint32_t* __restrict__ scratch) {
+  const uint32_t blk = blockIdx.x / MERKLE_SPLIT, sub = blockIdx.x % MERKLE_SPLIT;
+  const uint32_t off = offsets[blk];
+  const uint32_t total = offsets[blk + 1] - off;
+  if (total < 2) return;
+  const uint32_t H = merkle_split_height(total);
+  const uint32_t m = (total + (1u << H) - 1) >> H;
+  const uint32_t start = sub << H;
+  if (start >= total) return;  // all three returns are workgroup-uniform
+  const uint32_t c0 = min(1u << H, total - start);
+  uint32_t cnt = c0;
+  const uint32_t* src = leaves + (size_t)(off + start) * 8;
+  uint32_t* tree = scratch + (size_t)(off + start) * 8;
+  uint32_t level = 0;
+  int mut = 0;
+  while (cnt > 1) {
+    const uint32_t half = (cnt + 1) >> 1;
+    for (uint32_t base = 0; base < half; base += WG) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t o[8];
+      if (i < half) {
+        uint32_t a[8], b[8];
+        const uint32_t j = 2 * i + 1 < cnt ? 2 * i + 1 : cnt - 1;
+        load8(a, src + (size_t)(2 * i) * 8);
+        load8(b, src + (size_t)j * 8);
+        if (j != 2 * i) {
+          uint32_t diff = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) diff |= a[k] ^ b[k];
+          mut |= diff == 0;
+        }
+        sha256d_pair(o, a, b);
+      }
+      __syncthreads();
+      if (i < half) store8(tree + (size_t)i * 8, o);
+      __syncthreads();
+    }
+    src = tree;
+    cnt = half;
+    ++level;
+  }
+  mut = __syncthreads_or(mut);
+  if (threadIdx.x == 0) {
+    uint32_t x[8];
+    load8(x, src);
+    if (m > 1)
+      for (; level < H; ++level) sha256d_pair(x, x, x);
+    store8(tree, x);
+    if (c0 >= 2) tree[8] = (uint32_t)(mut != 0);
+  }
+}
+
+__global__ void __launch_bounds__(64) hkv_merkle_top_kernel(const uint32_t* __restrict__ leaves,
+                                                            const uint32_t* __restrict__ offsets,
+                                                            const uint32_t* __restrict__ scratch,
+                                                            uint32_t* __restrict__ roots,
+                                                            uint8_t* __restrict__ mutated) {
+  __shared__ uint32_t node[MERKLE_SPLIT][8];
+  const uint32_t blk = blockIdx.x;
+  const uint32_t off = offsets[blk];
+  const uint32_t total = offsets[blk + 1] - off;
+  const uint32_t t = threadIdx.x;
+  if (total < 2) {  // block-uniform
+    if (t == 0) {
+      uint32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (total == 1) load8(r, leaves + (size_t)off * 8);
+      store8(roots + (size_t)blk * 8, r);
+      mutated[blk] = 0;
+    }
+    return;
+  }
+  const uint32_t H = merkle_split_height(total);
+  uint32_t cnt = (total + (1u << H) - 1) >> H;
+  int mut = 0;
+  if (t < cnt) {
+    const uint32_t* p = scratch + (size_t)(off + (t << H)) * 8;
+    load8(node[t], p);
+    const uint32_t ct = min(1u << H, total - (t << H));
+    if (ct >= 2) mut = p[8] != 0;
+  }
+  __syncthreads();
+  while (cnt > 1) {  // at most 3 levels of <= 4 pairs
+    const uint32_t half = (cnt + 1) >> 1;
+    uint32_t o[8];
+    if (t < half) {
+      const uint32_t j = 2 * t + 1 < cnt ? 2 * t + 1 : cnt - 1;
+      if (j != 2 * t) {
+        uint32_t diff = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) diff |= node[2 * t][k] ^ node[j][k];
+        mut |= diff == 0;
+      }
+      sha256d_pair(o, node[2 * t], node[j]);
+    }
+    __syncthreads();
+    if (t < half)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) node[t][k] = o[k];
+    __syncthreads();
+    cnt = half;
+  }
+  mut = __syncthreads_or(mut);
+  if (t == 0) {
+    store8(roots + (size_t)blk * 8, node[0]);
+    mutated[blk] = (uint8_t)(mut != 0);
+  }
+}
+
 hipError_t launch_merkle(const uint8_t* leaves, const uint32_t* offsets, uint32_t n_blocks, uint8_t* scratch,
                          uint8_t* roots, uint8_t* mutated, hipStream_t st) {
   if (n_blocks == 0) return hipSuccess;
+  if (n_blocks <= 256) {  // fewer blocks than CUs: split each tree over MERKLE_SPLIT workgroups
+    hipLaunchKernelGGL(hkv_merkle_sub_kernel, dim3(n_blocks * MERKLE_SPLIT), dim3(WG), 0, st,
+                       reinterpret_cast<const uint32_t*>(leaves), offsets, reinterpret_cast<uint32_t*>(scratch));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(hkv_merkle_top_kernel, dim3(n_blocks), dim3(64), 0, st,
+                       reinterpret_cast<const uint32_t*>(leaves), offsets,
+                       reinterpret_cast<const uint32_t*>(scratch), reinterpret_cast<uint32_t*>(roots), mutated);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(hkv_merkle_kernel, dim3(n_blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(leaves),
                      offsets, reinterpret_cast<uint32_t*>(scratch), reinterpret_cast<uint32_t*>(roots), mutated);
   return hipGetLastError();
