@@ -10,14 +10,19 @@ construction (90% compressed / 10% uncompressed keys from a 65,536-key pool,
 low-S) and resident in HBM before the timed region. One step = the full
 verify of the rank's shard (prologue + ecmult + x-compare -> verdict bitmap)
 plus, for N > 1, the RCCL all-gather of the verdict bitmap (the only
-collective). value = all ranks' verifies / max-over-ranks time.
+collective; hkv/shard.py ShardedVerify). value = all ranks' verifies /
+max-over-ranks time.
 
-Also reported: verdict mismatches vs the construction labels (must be 0),
-the ecmult kernel's roofline (integer limb products per verify from
-hkv/opcount.py over the HIP-event-timed kernel duration, against the
-measured v_mad_u64_u32 peak), and the CPU baseline: the C restatement
-(oracle/, kind "port" — libsecp256k1 is not installed on the box) timed on the
-host cores on a bounded sample.
+Also reported (rank 0, N = 1): the ecmult kernel's roofline (the REFERENCE
+algorithm's limb products per verify, hkv/opcount.py P_ALG_ECMULT, over the
+HIP-event-timed launch, against the v_mad_u64_u32 peak at 2.4 GHz and at the
+measured mad rate and clock); configs[0] (the 2,000-tx P2PKH block), [2]
+(block mix) and [3] (adversarial 1M, every class of hkv/adversarial.py); and
+the CPU baseline leg: the C restatement (oracle/, kind "port") and OpenSSL's
+ECDSA_do_verify (the survey's labelled non-reference fallback; libsecp256k1 is
+not installed on the box), single-thread and on the job's CPU share, on the
+configs[0] block and on config-2 / adversarial samples, with their verdicts
+compared to the GPU's on the same records.
 """
 from __future__ import annotations
 
@@ -37,76 +42,169 @@ POOL = 65536
 UNC_PERMILLE = 100
 
 
-def cpu_baseline(records_host, threads: int):
-    """Time the C oracle (checker port of the reference semantics) on the host."""
-    import numpy as np
-    so = os.path.join(ROOT, "oracle", "build", "libhkv_oracle.so")
-    if not os.path.exists(so):
-        import subprocess
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    lib = ctypes.CDLL(so)
-    lib.hkvo_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
-                                      ctypes.c_int]
+def host_info() -> dict:
+    """lscpu model / topology of the box's host and this job's CPU share."""
+    import subprocess
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU max MHz"):
+                info[k.strip()] = v.strip()
+    except Exception:  # pragma: no cover
+        pass
+    return info
 
-    def run(n, t):
+
+def cpu_baseline(samples, threads: int) -> dict:
+    """The CPU leg (oracle/ is timed here and used as the checker here only).
+
+    samples: [(name, records uint8 [n*168], mode, gpu verdicts bool[n] or None,
+    repeat)]: each implementation verifies the sample on `threads` pthreads
+    (tiled `repeat` times so the run lasts long enough to time; its verdicts
+    on the sample are compared with the GPU's) and its first 4,096 records on
+    one thread.
+    Implementations: "port" = oracle/hkv_oracle.c (C restatement of the
+    reference semantics; no GLV, generic inversions), "openssl" = OpenSSL 3
+    ECDSA_do_verify behind the semantic adapter (oracle/openssl_check.c) —
+    the survey's labelled non-reference fallback, libsecp256k1 being absent."""
+    import numpy as np
+    import subprocess
+    ob = os.path.join(ROOT, "oracle", "build")
+    if not (os.path.exists(os.path.join(ob, "libhkv_oracle.so")) and os.path.exists(os.path.join(ob, "libhkv_openssl.so"))):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    port = ctypes.CDLL(os.path.join(ob, "libhkv_oracle.so"))
+    port.hkvo_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    ossl = ctypes.CDLL(os.path.join(ob, "libhkv_openssl.so"))
+    ossl.hkvo_openssl_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_int]
+    impls = {"port": port.hkvo_verify_batch, "openssl": ossl.hkvo_openssl_verify_batch}
+
+    def run(fn, recs, mode, t):
+        n = len(recs) // 168
         out = np.zeros(n, dtype=np.uint8)
         t0 = time.perf_counter()
-        lib.hkvo_verify_batch(ctypes.c_void_p(records_host.ctypes.data), n, 0, ctypes.c_void_p(out.ctypes.data), t)
-        dt = time.perf_counter() - t0
-        return n / dt, int(out.sum())
+        fn(ctypes.c_void_p(recs.ctypes.data), n, mode, ctypes.c_void_p(out.ctypes.data), t)
+        return n / (time.perf_counter() - t0), out.astype(bool)
 
-    n1 = 2048
-    st_rate, ok1 = run(n1, 1)
-    nm = min(len(records_host) // 168, 8192 * threads)
-    mt_rate, okm = run(nm, threads)
-    return {"value": round(mt_rate, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
-            "sample": f"{nm} of the timed config-2 records, HKV_LIBSECP semantics, {threads} pthreads "
-                      f"(oracle/hkv_oracle.c; libsecp256k1 absent on the box)",
-            "single_thread_value": round(st_rate, 1), "sample_accepts": okm, "sample_n": nm}
+    res = {}
+    for name, recs, mode, gpu, repeat in samples:
+        recs = np.ascontiguousarray(recs)
+        big = np.tile(recs, repeat) if repeat > 1 else recs
+        row = {"records": len(recs) // 168, "mode": "LIBSECP" if mode == 0 else "HASKOIN"}
+        n1 = min(len(recs) // 168, 4096)  # single-thread run: the first 4,096 records
+        for iname, fn in impls.items():
+            st, _ = run(fn, recs[: n1 * 168], mode, 1)
+            mt, vm = run(fn, big, mode, threads)
+            vm = vm[: len(recs) // 168]
+            row[iname] = {"1_thread": round(st, 1), f"{threads}_threads": round(mt, 1),
+                          "accepts": int(vm.sum())}
+            if gpu is not None:
+                row[iname]["mismatches_vs_gpu"] = int((vm != gpu).sum())
+        res[name] = row
+    c0 = res.get("config0_block", {})
+    best = max(("port", "openssl"), key=lambda k: c0.get(k, {}).get(f"{threads}_threads", 0.0))
+    return {"value": c0.get(best, {}).get(f"{threads}_threads"), "unit": "verifies/s", "cores": threads,
+            "kind": "port",
+            "impl": best,
+            "sample": f"BASELINE configs[0]: the 4,000 inputs of the 2,000-tx P2PKH block (records extracted on "
+                      f"device, HKV_HASKOIN = verifyHashSig), tiled x{threads} for the {threads}-thread run; "
+                      f"the faster of the C restatement (port) and OpenSSL ECDSA_do_verify; libsecp256k1 is "
+                      f"not installed on the box",
+            "single_thread_value": c0.get(best, {}).get("1_thread"),
+            "samples": res, "host": host_info()}
 
 
-def block_mix(v, torch, sptr, steps: int) -> dict:
+def _time_block(v, torch, db, bstream, k: int) -> dict:
+    """Verify one HBM-resident tx batch end to end (tx index, sighash, DER /
+    template / HASH160 checks, ECDSA) on bstream; HIP-event times."""
+    import numpy as np
+    sptr = bstream.cuda_stream
+
+    def run():
+        v.verify_std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(),
+                                   db.bits.data_ptr(), sptr)
+
+    def extract():
+        v.std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(), sptr)
+
+    run()
+    torch.cuda.synchronize()
+    words = db.bits.cpu().numpy().view("uint32")
+    got = np.unpackbits(words.view(np.uint8), bitorder="little")[:db.n].astype(bool)
+    res = {"txs": db.n_tx, "inputs": db.n, "tx_bytes": int(db.d_bytes.numel()),
+           "accepted": int(got.sum()), "rejected": int(db.n - got.sum())}
+    for name, fn in (("total", run), ("extract_sighash", extract)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(bstream)
+        for _ in range(k):
+            fn()
+        e1.record(bstream)
+        torch.cuda.synchronize()
+        res[f"{name}_us"] = round(e0.elapsed_time(e1) * 1e3 / k, 1)
+    res["inputs_per_s"] = round(db.n / (res["total_us"] * 1e-6), 1)
+    return res, got
+
+
+def block_mix(v, torch, steps: int) -> dict:
     """BASELINE configs[2]: a 2,000-tx P2PKH + P2WPKH block verified end to
-    end on device (tx index, legacy / BIP143 sighash, DER + HASH160 template
-    checks, ECDSA) from HBM-resident tx bytes; plus the same pipeline on a
-    32-block batch (64,000 txs) for its throughput."""
+    end on device from HBM-resident tx bytes; plus the same pipeline on a
+    32-block batch (64,000 txs) for its throughput. Every generated input is
+    valid; `rejected` must be 0 (the per-input records are checked against the
+    oracle byte for byte in tests/test_gpu_sighash.py, not here)."""
     from hkv import blockgen
     out = {}
-    # a dedicated stream: torch's default stream is the null stream (pointer 0),
-    # which libhkv would replace by its own stream and the events would miss
+    # a dedicated stream: torch's default stream is the null stream (pointer 0)
     bstream = torch.cuda.Stream()
-    sptr = bstream.cuda_stream
     for label, n_tx in (("block", 2000), ("batch32", 64000)):
         txs, inputs = blockgen.make_block(v, torch, n_tx=n_tx, seed=blockgen.SEED + n_tx)
         db = blockgen.DeviceBlock(torch, txs, inputs)
-
-        def run():
-            v.verify_std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(),
-                                       db.bits.data_ptr(), sptr)
-
-        def extract():
-            v.std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(), sptr)
-
-        run()
-        torch.cuda.synchronize()
-        words = db.bits.cpu().numpy().view("uint32")
-        import numpy as np
-        accepted = int(np.unpackbits(words.view(np.uint8), bitorder="little")[:db.n].sum())
-        res = {"txs": n_tx, "inputs": db.n, "tx_bytes": int(db.d_bytes.numel()), "mismatches": db.n - accepted}
-        for name, fn in (("total", run), ("extract_sighash", extract)):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            k = max(3, steps // (1 if label == "block" else 4))
-            e0.record(bstream)
-            for _ in range(k):
-                fn()
-            e1.record(bstream)
-            torch.cuda.synchronize()
-            res[f"{name}_us"] = round(e0.elapsed_time(e1) * 1e3 / k, 1)
-        res["inputs_per_s"] = round(db.n / (res["total_us"] * 1e-6), 1)
-        out[label] = res
+        out[label], _ = _time_block(v, torch, db, bstream, max(3, steps // (1 if label == "block" else 4)))
     out["workload"] = ("BASELINE configs[2]: 60% P2WPKH (BIP143) / 40% P2PKH (legacy) inputs, 1-3 inputs and 2 "
                        "outputs per tx, SIGHASH_ALL; verifyStdInput semantics, tx bytes resident in HBM")
     return out
+
+
+def config0_block(v, torch, steps: int):
+    """BASELINE configs[0] on the GPU: the 2,000-tx x 2-input x 2-output P2PKH
+    block (seed 0x484B5631, 4,096-key pool) verified end to end from
+    HBM-resident tx bytes. Returns (result, device-extracted records, GPU
+    verdicts, txs, inputs); the CPU leg times the same inputs on the host."""
+    from hkv import blockgen
+    txs, inputs = blockgen.make_p2pkh_block(v, torch)
+    db = blockgen.DeviceBlock(torch, txs, inputs)
+    bstream = torch.cuda.Stream()
+    res, got = _time_block(v, torch, db, bstream, max(5, steps))
+    recs = db.records[: db.n * 168].cpu().numpy().copy()
+    res["workload"] = ("BASELINE configs[0]: 2,000 txs x 2 P2PKH inputs x 2 P2PKH outputs = 4,000 signatures, "
+                       "seed 0x484B5631, compressed keys from a 4,096-key pool, SIGHASH_ALL, low S; "
+                       "verifyStdInput semantics end to end on device")
+    return res, recs, got, txs, inputs
+
+
+def cpu_sighash_leg(txs, inputs, gpu_records) -> dict:
+    """Host side of configs[0]'s sighash (the CPU leg): the Python restatement
+    of verifyStdInput's non-ECDSA half (tx parse, txSigHash, decodeTxSig,
+    HASH160 template check; oracle/sighash_oracle.py) over the block's inputs,
+    timed single-threaded, and its records compared byte for byte with the
+    GPU's (msg32 = the sighash)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sighash_oracle as sh
+    t0 = time.perf_counter()
+    parsed = [sh.tx_parse(t) for t in txs]
+    exp = b"".join(sh.std_input_record(parsed[t], i, p, val) for (t, i, p, val) in inputs)
+    dt = time.perf_counter() - t0
+    got = gpu_records.tobytes()
+    n = len(inputs)
+    rec_mism = sum(got[k * 168:(k + 1) * 168] != exp[k * 168:(k + 1) * 168] for k in range(n))
+    msg_mism = sum(got[k * 168:k * 168 + 32] != exp[k * 168:k * 168 + 32] for k in range(n))
+    return {"inputs": n, "inputs_per_s_1_thread": round(n / dt, 1), "record_mismatches_vs_gpu": int(rec_mism),
+            "msg32_mismatches_vs_gpu": int(msg_mism), "impl": "oracle/sighash_oracle.py (Python, 1 thread)"}
 
 
 def host_path(v, recs, n: int, steps: int) -> dict:
@@ -187,21 +285,33 @@ def header_batches(v, torch, steps: int) -> dict:
     return out
 
 
-def adversarial_mix(v, torch, recs, n: int, sptr: int, steps: int) -> dict:
-    """BASELINE configs[3]: the timed batch with 30% of its records mutated into
-    the SURVEY §8(c) invalid classes (hkv/adversarial.py: labels fixed by
-    construction), verified in both modes; mismatches must be 0."""
+def adversarial_mix(v, torch, n: int, sptr: int, steps: int):
+    """BASELINE configs[3]: 1,048,576 generated records (seed 0x484B5634), 30%
+    of them mutated evenly into every invalid class of hkv/adversarial.py and
+    5% into its special valid classes (labels fixed by construction, checked
+    against the C restatement and OpenSSL in the tests and in the CPU leg
+    here); verified in both modes; mismatches vs the labels must be 0."""
     import numpy as np
     from hkv import adversarial
-    adv, lab_lib, lab_hask, _ = adversarial.mutate(recs.cpu().numpy(), seed=0x484B5634)
-    d = torch.from_numpy(adv).to(recs.device)
-    words = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device=recs.device)
+    seed = 0x484B5634
+    d = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
+    v.gen_records_device(0, seed, n, POOL, UNC_PERMILLE, d.data_ptr(), sptr)
+    t = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
+    v.gen_records_device(0, seed, n, POOL, 1000, t.data_ptr(), sptr)  # same records, 65-byte keys (y source)
+    torch.cuda.synchronize()
+    adv, lab_lib, lab_hask, cls = adversarial.mutate(d.cpu().numpy(), seed=seed, twin=t.cpu().numpy())
+    del t
+    d.copy_(torch.from_numpy(adv))
+    words = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device=d.device)
     stream = torch.cuda.current_stream()
-    out = {"records": n, "invalid_frac": round(float(1 - lab_lib.mean()), 4)}
+    out = {"records": n, "invalid_frac": round(float(np.isin(cls, np.arange(len(adversarial.INVALID_CLASSES))).mean()), 4),
+           "special_valid_frac": round(float((cls >= len(adversarial.INVALID_CLASSES)).mean()), 4)}
+    verdicts = {}
     for name, mode, lab in (("libsecp", 0, lab_lib), ("haskoin", 1, lab_hask)):
         v.verify_device(0, d.data_ptr(), n, mode, words.data_ptr(), sptr)
         torch.cuda.synchronize()
         got = adversarial.unpack_bits(words.cpu().numpy().view(np.uint32), n)
+        verdicts[mode] = got
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         k = max(3, steps // 2)
         e0.record(stream)
@@ -210,11 +320,12 @@ def adversarial_mix(v, torch, recs, n: int, sptr: int, steps: int) -> dict:
         e1.record(stream)
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / k
-        out[name] = {"mismatches": int((got != lab).sum()), "accepts": int(got.sum()),
+        out[name] = {"mismatches_vs_labels": int((got != lab).sum()), "accepts": int(got.sum()),
                      "ms": round(ms, 4), "verifies_per_s": round(n / (ms * 1e-3), 1)}
-    out["workload"] = ("BASELINE configs[3]: msg-bit / r=0 / s>=n / bad prefix / x>=p / high-S mutations of "
-                       "the config-2 records, labels by construction")
-    return out
+    out["workload"] = ("BASELINE configs[3]: 30% invalid, evenly: " + ", ".join(
+        c for c, _, _ in adversarial.INVALID_CLASSES) + "; 5% special valid: reencode, valid_hybrid, r+n branch, "
+        "edge u1/u2, u1=0, msg32>=n, ladder collisions; labels by construction")
+    return out, adv, verdicts
 
 
 def merkle_batches(v, torch, steps: int) -> dict:
@@ -255,8 +366,28 @@ def merkle_batches(v, torch, steps: int) -> dict:
                       "blocks_per_s": round(nb / (us * 1e-6), 1), "nodes_per_s": round(nodes / (us * 1e-6), 1),
                       "mutated": int(dm.sum().item())}
     out["workload"] = ("buildMerkleRoot per block (NodeSpec.hs:185-193 / haskoin-core Merkle [dep]), random "
-                       "txids resident in HBM, one workgroup per block")
+                       "txids resident in HBM; <= n_cu blocks: 8 subtree workgroups per block + a top join, "
+                       "more: one workgroup per block")
     return out
+
+
+def load_traffic(path: str, n: int):
+    """HBM bytes per ecmult launch from the committed PMC summary
+    (tools/pmc_summary.py): FETCH_SIZE x 2 (MI355X_MICROARCH.md: on gfx950
+    FETCH_SIZE reports 1/2 of the bytes of wide reads) + WRITE_SIZE, both KB
+    counters x 1024, separate --pmc passes of the same 1M-record launch."""
+    if not os.path.exists(path):
+        return None, None
+    try:
+        tj = json.load(open(path))
+    except Exception:
+        return None, None
+    if tj.get("per_verify_records") != n:
+        return None, None
+    f, w = tj.get("fetch_bytes_per_launch"), tj.get("write_bytes_per_launch")
+    if f is None or w is None:
+        return None, None
+    return 2 * f + w, {"fetch_size_bytes": f, "write_size_bytes": w, "source": tj.get("source")}
 
 
 def main() -> None:
@@ -268,6 +399,7 @@ def main() -> None:
     ap.add_argument("--mode", type=int, default=0, help="0 = HKV_LIBSECP, 1 = HKV_HASKOIN")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-block-mix", action="store_true")
+    ap.add_argument("--no-config0", action="store_true")
     ap.add_argument("--no-adversarial", action="store_true")
     ap.add_argument("--no-headers", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
@@ -291,11 +423,9 @@ def main() -> None:
 
     import hkv
     from hkv import opcount
-    from hkv.shard import assemble_bitmap, shard_bounds
+    from hkv.shard import ShardedVerify
 
     n_total = args.per_gpu * world
-    lo, hi = shard_bounds(n_total, rank, world)
-    n = hi - lo
     v = hkv.Verifier(hkv.VerifierConfig(device_ids=[local]))
     # a real (non-null) stream made current: libhkv enqueues on it and the RCCL
     # all-gather, which waits on torch's current stream, is ordered after the
@@ -303,21 +433,19 @@ def main() -> None:
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+
+    def verify_shard(lo, hi, bits):
+        v.verify_device(0, recs.data_ptr(), hi - lo, args.mode, bits.data_ptr(), sptr)
+
+    sv = ShardedVerify(torch, n_total, rank, world, verify_shard, dist=dist)
+    n = sv.local_n
     recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
     # each rank generates exactly its slice of the global synthetic batch
-    v.gen_records_device(0, SEED + lo, n, POOL, UNC_PERMILLE, recs.data_ptr(), sptr)
-    words_per_rank = (args.per_gpu + 63) // 64 * 2 + 2
-    bits = torch.zeros(words_per_rank, dtype=torch.int32, device="cuda")
-    gathered = torch.zeros(words_per_rank * world, dtype=torch.int32, device="cuda")
+    v.gen_records_device(0, SEED + sv.lo, n, POOL, UNC_PERMILLE, recs.data_ptr(), sptr)
     torch.cuda.synchronize()
 
-    def step():
-        v.verify_device(0, recs.data_ptr(), n, args.mode, bits.data_ptr(), sptr)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, bits)
-
     for _ in range(args.warmup):
-        step()
+        sv.step()
     torch.cuda.synchronize()
     v.lib.hkv_profile_enable(v.ctx, 1)
     if world > 1:
@@ -325,13 +453,15 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        sv.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     pm, em, nl = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
     v.lib.hkv_profile_read(v.ctx, 0, ctypes.byref(pm), ctypes.byref(em), ctypes.byref(nl))
+    sclk = ctypes.c_double()
+    v.lib.hkv_profile_clock(v.ctx, 0, ctypes.byref(sclk))
     v.lib.hkv_profile_enable(v.ctx, 0)
 
     t = torch.tensor([dt, em.value / max(1, nl.value), pm.value / max(1, nl.value)], dtype=torch.float64,
@@ -340,48 +470,54 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max, ecm_ms, pro_ms = t.tolist()
 
-    # correctness on the timed batch: every constructed signature is valid
-    words = (gathered if world > 1 else bits).cpu().numpy().view(np.uint32)
-    if world > 1:
-        full = assemble_bitmap(n_total, world, words, words_per_rank)
-    else:
-        full = words[: (n + 31) // 32]
+    # every constructed signature of the timed batch is valid (construction
+    # labels; the GPU verdicts are compared with CPU implementations on a
+    # sample of these records in the CPU leg below)
+    full = sv.bitmap()
     accepted = int(np.unpackbits(full.view(np.uint8), bitorder="little")[:n_total].sum())
     mismatches = n_total - accepted
 
     if rank == 0:
         value = n_total * args.steps / dt_max
-        per_launch_products = opcount.ECMULT_PRODUCTS_PER_VERIFY * n
-        achieved = per_launch_products / (ecm_ms * 1e-3) / 1e12
+        per_launch = n
+        achieved = opcount.P_ALG_ECMULT * per_launch / (ecm_ms * 1e-3) / 1e12
+        achieved_impl = opcount.ECMULT_PRODUCTS_PER_VERIFY * per_launch / (ecm_ms * 1e-3) / 1e12
         peak = opcount.PEAK_PRODUCTS_PER_S / 1e12
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                if tj.get("per_verify_records") == n:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        mix = None
+        f_mhz = sclk.value if 500.0 < sclk.value < 4000.0 else None
+        peak_meas = opcount.R_MUL_MEASURED * opcount.N_CU * f_mhz * 1e6 / 1e12 if f_mhz else None
+        traffic, traffic_raw = load_traffic(args.traffic_json, n)
+        c0 = mix = hp = hdr = mkl = adv = None
+        c0_recs = c0_got = c0_txs = c0_inputs = adv_recs = adv_got = None
+        if world == 1 and not args.no_config0:
+            c0, c0_recs, c0_got, c0_txs, c0_inputs = config0_block(v, torch, args.steps)
         if world == 1 and not args.no_block_mix:
-            mix = block_mix(v, torch, sptr, args.steps)
-        hp = None
+            mix = block_mix(v, torch, args.steps)
         if world == 1 and not args.no_host_path:
             hp = host_path(v, recs, n, args.steps)
-        hdr = None
         if world == 1 and not args.no_headers:
             hdr = header_batches(v, torch, args.steps)
-        mkl = None
         if world == 1 and not args.no_merkle:
             mkl = merkle_batches(v, torch, args.steps)
-        adv = None
         if world == 1 and not args.no_adversarial:
-            adv = adversarial_mix(v, torch, recs, n, sptr, args.steps)
+            adv, adv_recs, adv_got = adversarial_mix(v, torch, n, sptr, args.steps)
         cpu = None
         if not args.no_cpu_baseline:
-            host = recs[: min(n, 8192 * 16) * 168].cpu().numpy()
-            threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(host, threads)
+            threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                                 else (os.cpu_count() or 1)))
+            samples = []
+            if c0_recs is not None:
+                samples.append(("config0_block", c0_recs, 1, c0_got, threads))
+            m2 = min(n, 16384)
+            gpu2 = np.unpackbits(full[: (m2 + 31) // 32].view(np.uint8), bitorder="little")[:m2].astype(bool)
+            samples.append(("config1_sample", recs[: m2 * 168].cpu().numpy(), args.mode, gpu2, max(1, threads // 2)))
+            if adv_recs is not None:
+                m4 = min(n, 16384)
+                for mode in (0, 1):
+                    samples.append((f"config3_sample_{'libsecp' if mode == 0 else 'haskoin'}",
+                                    adv_recs[: m4 * 168], mode, adv_got[mode][:m4], max(1, threads // 2)))
+            cpu = cpu_baseline(samples, threads)
+            if c0_recs is not None:
+                cpu["config0_host_sighash"] = cpu_sighash_leg(c0_txs, c0_inputs, c0_recs)
         line = {
             "metric": "ECDSA verifies/sec (1/8 GPU) + verdict mismatches vs libsecp256k1",
             "value": round(value, 1),
@@ -401,13 +537,29 @@ def main() -> None:
                        "global_batch": n_total, "per_gpu": n, "mode": "LIBSECP" if args.mode == 0 else "HASKOIN",
                        "parallelism": f"dp{world}"},
             "mismatches": mismatches,
+            "mismatches_note": "timed batch vs construction labels (all valid); GPU vs CPU implementations on "
+                               "the same records: cpu_baseline.samples.*.*.mismatches_vs_gpu",
             "kernel_ms": {"prologue": round(pro_ms, 4), "ecmult": round(ecm_ms, 4)},
             "roofline": {"bound": "valu_int", "achieved": round(achieved, 4), "peak": round(peak, 3),
                          "unit": "T limb-products/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
                          "traffic": traffic,
                          "kernel": "hkv_ecmult_kernel",
-                         "products_per_verify": opcount.ECMULT_PRODUCTS_PER_VERIFY},
+                         "p_alg": opcount.P_ALG_ECMULT,
+                         "p_alg_note": "reference algorithm (libsecp256k1 ecmult: GLV + wNAF5 Q, w=15 G tables, "
+                                       "129 doublings) priced in 32x32 limb products; frozen (hkv/opcount.py)",
+                         "p_impl": opcount.ECMULT_PRODUCTS_PER_VERIFY,
+                         "achieved_impl": round(achieved_impl, 4),
+                         "frac_nominal": round(achieved / peak, 4),
+                         "sclk_mhz": round(f_mhz, 1) if f_mhz else None,
+                         "peak_measured_clock": round(peak_meas, 3) if peak_meas else None,
+                         "frac_measured_clock": round(achieved / peak_meas, 4) if peak_meas else None,
+                         "measured_rate_note": "57.07 lane-products/clk/CU (profiles/r01_ubench_int.json) x 256 "
+                                               "CUs x the clock block 0 of the launch ran at (clock64/wall_clock64)",
+                         "traffic_raw": traffic_raw,
+                         "traffic_note": "HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE "
+                                         "halving, MI355X_MICROARCH.md); algorithmic input = 168 B/verify"},
             "cpu_baseline": cpu,
+            "config0": c0,
             "block_mix": mix,
             "adversarial": adv,
             "headers": hdr,

@@ -51,6 +51,13 @@ struct DevCtx {
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
+  unsigned long long* clk = nullptr;  // ecmult clock probe (4 counters)
+  int wall_khz = 0;                   // constant-rate counter frequency
+  // The scratch above (im, bits, qs, txt, pool, staging) is shared by every
+  // call on this device whatever stream it names: each call waits for the
+  // previous user's work (this event) before enqueueing and records it after,
+  // so calls on different streams run in enqueue order instead of racing.
+  hipEvent_t last_use = nullptr;
 };
 
 }  // namespace
@@ -98,6 +105,17 @@ int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
   return HKV_OK;
 }
 
+// Order a call on stream st after the previous user of the device's scratch
+// (acquire) and publish st as the new last user (release). Callers hold ctx->mu.
+int scratch_acquire(DevCtx& d, hipStream_t st) {
+  HKV_TRY(hipStreamWaitEvent(st, d.last_use, 0), "hipStreamWaitEvent(scratch)");
+  return HKV_OK;
+}
+int scratch_release(DevCtx& d, hipStream_t st) {
+  HKV_TRY(hipEventRecord(d.last_use, st), "hipEventRecord(scratch)");
+  return HKV_OK;
+}
+
 // enqueue prologue + ecmult for n records at d_records; verdict words in d.bits
 int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st) {
   const size_t n_pad = round_up(n, hkv::WG);
@@ -121,7 +139,8 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
   const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
-  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, d.bits, split, st),
+  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, d.bits, split,
+                             d.profile ? d.clk : nullptr, st),
           "ecmult launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
@@ -142,6 +161,10 @@ int init_device(DevCtx& d, int device) {
   d.n_cu = prop.multiProcessorCount;
   HKV_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
   HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
+  HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
+  HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
+  HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
+  HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
   HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 64 MiB at radix 2^20
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
@@ -175,6 +198,8 @@ void free_device(DevCtx& d) {
   for (auto p : d.stage)
     if (p) (void)hipFree(p);
   if (d.hbits) (void)hipHostFree(d.hbits);
+  if (d.clk) (void)hipFree(d.clk);
+  if (d.last_use) (void)hipEventDestroy(d.last_use);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   if (d.copy_stream) (void)hipStreamDestroy(d.copy_stream);
   d = DevCtx();
@@ -196,7 +221,8 @@ int self_check(DevCtx& d) {
   const size_t n = 256;
   uint8_t* recs = nullptr;
   HKV_TRY(hipMalloc(&recs, n * hkv::REC_SIZE), "hipMalloc(selfcheck)");
-  int rc = ensure_pool(d, 0x484B5630ull, 16, d.stream);
+  int rc = scratch_acquire(d, d.stream);
+  if (!rc) rc = ensure_pool(d, 0x484B5630ull, 16, d.stream);
   if (!rc) {
     hipError_t e = hkv::launch_gen_records(0x484B5630ull, (uint32_t)n, d.pool, d.pool_n, 250, recs, d.stream);
     if (e != hipSuccess) rc = hip_fail(e, "selfcheck gen");
@@ -208,6 +234,7 @@ int self_check(DevCtx& d) {
     if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess) rc = hip_fail(e, "selfcheck copy");
   }
+  if (!rc) rc = scratch_release(d, d.stream);
   (void)hipFree(recs);
   if (rc) return rc;
   for (uint32_t w : words)
@@ -360,6 +387,19 @@ void hkv_batch_free(hkv_batch* b) {
 uint8_t* hkv_batch_records(hkv_batch* b) { return b ? b->host : nullptr; }
 size_t hkv_batch_capacity(const hkv_batch* b) { return b ? b->cap : 0; }
 
+// On an error part-way through a multi-device call, wait for every device
+// already touched (0..k) before returning: their async H2D copies still read
+// the caller's host records and their kernels still write d.hbits.
+static int fail_sync(hkv_ctx* ctx, size_t k, int rc) {
+  for (size_t j = 0; j <= k && j < ctx->devs.size(); ++j) {
+    DevCtx& d = ctx->devs[j];
+    (void)hipSetDevice(d.device);
+    (void)hipStreamSynchronize(d.copy_stream);
+    (void)hipStreamSynchronize(d.stream);
+  }
+  return rc;
+}
+
 static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_t mode, uint32_t* out) {
   if (!ctx || !host || !out || mode > HKV_MODE_HASKOIN) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
@@ -385,23 +425,27 @@ static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_
     DevCtx& d = ctx->devs[k];
     const size_t len = shards[k].hi - shards[k].lo;
     if (!len) continue;
-    HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-    if (d.recs_cap < len) {
+    hipError_t e0 = hipSetDevice(d.device);
+    int rc = e0 == hipSuccess ? scratch_acquire(d, d.stream) : hip_fail(e0, "hipSetDevice");
+    if (!rc) rc = scratch_acquire(d, d.copy_stream);
+    if (!rc && d.recs_cap < len) {
       if (d.recs) (void)hipFree(d.recs);
       d.recs = nullptr;
       d.recs_cap = 0;
-      HKV_TRY(hipMalloc(&d.recs, len * hkv::REC_SIZE), "hipMalloc(records)");
-      d.recs_cap = len;
+      e0 = hipMalloc(&d.recs, len * hkv::REC_SIZE);
+      if (e0 != hipSuccess) rc = hip_fail(e0, "hipMalloc(records)");
+      else d.recs_cap = len;
     }
     const size_t words = (len + 31) / 32;
-    if (d.hbits_cap < words) {
+    if (!rc && d.hbits_cap < words) {
       if (d.hbits) (void)hipHostFree(d.hbits);
       d.hbits = nullptr;
       d.hbits_cap = 0;
-      HKV_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.hbits), words * 4, hipHostMallocPortable),
-              "hipHostMalloc(bits)");
-      d.hbits_cap = words;
+      e0 = hipHostMalloc(reinterpret_cast<void**>(&d.hbits), words * 4, hipHostMallocPortable);
+      if (e0 != hipSuccess) rc = hip_fail(e0, "hipHostMalloc(bits)");
+      else d.hbits_cap = words;
     }
+    if (rc) return fail_sync(ctx, k, rc);
     // Pipelined over chunks of whole resident grids: the copy stream moves
     // chunk c+1 over PCIe while the verify stream works on chunk c (events
     // order each verify after its own H2D); each chunk's verdict words go to
@@ -415,27 +459,31 @@ static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_
                              : len;
     const uint8_t* src = host + shards[k].lo * hkv::REC_SIZE;
     std::vector<hipEvent_t>& evs = h2d_events[k];
-    int rc = HKV_OK;
     for (size_t off = 0; off < len && !rc; off += chunk) {
       const size_t cl = std::min(chunk, len - off);
       hipEvent_t ev = nullptr;
-      HKV_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-      evs.push_back(ev);
-      HKV_TRY(hipMemcpyAsync(d.recs + off * hkv::REC_SIZE, src + off * hkv::REC_SIZE, cl * hkv::REC_SIZE,
-                             hipMemcpyHostToDevice, d.copy_stream),
-              "H2D records");
-      HKV_TRY(hipEventRecord(ev, d.copy_stream), "hipEventRecord");
-      HKV_TRY(hipStreamWaitEvent(d.stream, ev, 0), "hipStreamWaitEvent");
+      hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e == hipSuccess) evs.push_back(ev);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d.recs + off * hkv::REC_SIZE, src + off * hkv::REC_SIZE, cl * hkv::REC_SIZE,
+                           hipMemcpyHostToDevice, d.copy_stream);
+      if (e == hipSuccess) e = hipEventRecord(ev, d.copy_stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(d.stream, ev, 0);
+      if (e != hipSuccess) {
+        rc = hip_fail(e, "H2D records");
+        break;
+      }
       rc = enqueue_verify(d, d.recs + off * hkv::REC_SIZE, cl, mode, d.stream);
-      if (!rc)
-        HKV_TRY(hipMemcpyAsync(d.hbits + off / 32, d.bits, (cl + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream),
-                "D2H bits");
+      if (!rc) {
+        e = hipMemcpyAsync(d.hbits + off / 32, d.bits, (cl + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream);
+        if (e != hipSuccess) rc = hip_fail(e, "D2H bits");
+      }
     }
-    if (rc) {
-      (void)hipStreamSynchronize(d.copy_stream);
-      (void)hipStreamSynchronize(d.stream);
-      return rc;
-    }
+    // the copy stream must not run ahead into the next call's H2D while this
+    // call's verify still reads d.recs: it is ordered through last_use
+    if (!rc) rc = scratch_release(d, d.stream);
+    if (!rc) rc = scratch_acquire(d, d.copy_stream);
+    if (rc) return fail_sync(ctx, k, rc);
   }
   for (size_t k = 0; k < nd; ++k) {
     DevCtx& d = ctx->devs[k];
@@ -469,11 +517,12 @@ int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, ui
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
-  int rc = enqueue_verify(d, d_records, n, mode, st);
+  int rc = scratch_acquire(d, st);
+  if (!rc) rc = enqueue_verify(d, d_records, n, mode, st);
   if (rc) return rc;
   const size_t words = (n + 31) / 32;
   HKV_TRY(hipMemcpyAsync(d_bits, d.bits, words * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
-  return HKV_OK;
+  return scratch_release(d, st);
 }
 
 int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
@@ -486,11 +535,12 @@ int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint3
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
-  int rc = ensure_pool(d, seed ^ 0x706F6F6Cull, pool_size, st);
+  int rc = scratch_acquire(d, st);
+  if (!rc) rc = ensure_pool(d, seed ^ 0x706F6F6Cull, pool_size, st);
   if (rc) return rc;
   HKV_TRY(hkv::launch_gen_records(seed, (uint32_t)n, d.pool, d.pool_n, uncompressed_permille, d_records, st),
           "gen records launch");
-  return HKV_OK;
+  return scratch_release(d, st);
 }
 
 int hkv_debug_op(hkv_ctx* ctx, int dev, uint32_t op, size_t n, const uint32_t* d_a, const uint32_t* d_b,
@@ -538,6 +588,19 @@ int hkv_profile_read(hkv_ctx* ctx, int dev, double* prologue_ms, double* ecmult_
   return HKV_OK;
 }
 
+int hkv_profile_clock(hkv_ctx* ctx, int dev, double* sclk_mhz) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !sclk_mhz) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  HKV_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  unsigned long long c[4] = {0, 0, 0, 0};
+  HKV_TRY(hipMemcpy(c, d.clk, sizeof(c), hipMemcpyDeviceToHost), "D2H clock probe");
+  *sclk_mhz = 0;
+  if (c[3] > c[1] && d.wall_khz > 0) *sclk_mhz = (double)(c[2] - c[0]) / ((double)(c[3] - c[1]) / (d.wall_khz * 1e-3));
+  return HKV_OK;
+}
+
 int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_sighash_job* d_jobs, size_t n,
                        int32_t forkid, uint8_t* d_out, size_t out_stride, uint8_t* d_status, void* hip_stream) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || out_stride < 32 || out_stride % 4 ||
@@ -549,12 +612,13 @@ int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_si
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
-  int rc = enqueue_tx_index(d, d_txs, st);
+  int rc = scratch_acquire(d, st);
+  if (!rc) rc = enqueue_tx_index(d, d_txs, st);
   if (rc) return rc;
   HKV_TRY(hkv::launch_sighash(d_txs->bytes, d_txs->n_tx, d.txt, d_txs->scripts, d_txs->scripts_len, d_jobs,
                               (uint32_t)n, forkid, d_out, (uint32_t)out_stride, d_status, st),
           "sighash launch");
-  return HKV_OK;
+  return scratch_release(d, st);
 }
 
 int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, size_t n, int32_t forkid,
@@ -567,7 +631,8 @@ int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, s
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hkv_txs dt;
   void* djobs = nullptr;
-  int rc = stage_txs(d, txs, jobs, n * sizeof(hkv_sighash_job), &dt, &djobs);
+  int rc = scratch_acquire(d, d.stream);
+  if (!rc) rc = stage_txs(d, txs, jobs, n * sizeof(hkv_sighash_job), &dt, &djobs);
   if (!rc) rc = grow(&d.stage[4], &d.stage_cap[4], n * 33, "hipMalloc(sighash out)");
   if (!rc) rc = enqueue_tx_index(d, &dt, d.stream);
   if (rc) return rc;
@@ -579,7 +644,7 @@ int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, s
   HKV_TRY(hipMemcpyAsync(out32, dout, n * 32, hipMemcpyDeviceToHost, d.stream), "D2H sighash");
   if (status) HKV_TRY(hipMemcpyAsync(status, dout + n * 32, n, hipMemcpyDeviceToHost, d.stream), "D2H status");
   HKV_TRY(hipStreamSynchronize(d.stream), "sighash sync");
-  return HKV_OK;
+  return scratch_release(d, d.stream);
 }
 
 int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
@@ -591,7 +656,10 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
-  return enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
+  int rc = scratch_acquire(d, st);
+  if (!rc) rc = enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
+  if (!rc) rc = scratch_release(d, st);
+  return rc;
 }
 
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
@@ -603,11 +671,12 @@ int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, co
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
-  int rc = enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
+  int rc = scratch_acquire(d, st);
+  if (!rc) rc = enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
   if (!rc) rc = enqueue_verify(d, d_records, n, HKV_MODE_HASKOIN, st);
   if (rc) return rc;
   HKV_TRY(hipMemcpyAsync(d_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
-  return HKV_OK;
+  return scratch_release(d, st);
 }
 
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
@@ -620,7 +689,8 @@ int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job*
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hkv_txs dt;
   void* djobs = nullptr;
-  int rc = stage_txs(d, txs, jobs, n * sizeof(hkv_input_job), &dt, &djobs);
+  int rc = scratch_acquire(d, d.stream);
+  if (!rc) rc = stage_txs(d, txs, jobs, n * sizeof(hkv_input_job), &dt, &djobs);
   if (!rc && d.recs_cap < n) {
     if (d.recs) (void)hipFree(d.recs);
     d.recs = nullptr;
@@ -633,7 +703,7 @@ int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job*
   if (rc) return rc;
   HKV_TRY(hipMemcpyAsync(verdict_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
   HKV_TRY(hipStreamSynchronize(d.stream), "std inputs sync");
-  return HKV_OK;
+  return scratch_release(d, d.stream);
 }
 
 int hkv_gen_keys_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint8_t* d_priv, uint8_t* d_pub,
@@ -690,7 +760,8 @@ int hkv_check_headers(hkv_ctx* ctx, const uint8_t* headers, size_t n, const uint
   DevCtx& d = ctx->devs[0];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   // one staging buffer: limit (32) | prev (32) | headers (n*80) | hashes (n*32) | status (n)
-  int rc = grow(&d.stage[5], &d.stage_cap[5], 64 + n * 113, "hipMalloc(header batch)");
+  int rc = scratch_acquire(d, d.stream);
+  if (!rc) rc = grow(&d.stage[5], &d.stage_cap[5], 64 + n * 113, "hipMalloc(header batch)");
   if (rc) return rc;
   uint8_t* b = static_cast<uint8_t*>(d.stage[5]);
   uint8_t *dlim = b, *dprev = b + 32, *dh = b + 64, *dhash = dh + n * 80, *dst = dhash + n * 32;
@@ -702,7 +773,7 @@ int hkv_check_headers(hkv_ctx* ctx, const uint8_t* headers, size_t n, const uint
   HKV_TRY(hipMemcpyAsync(hashes_out, dhash, n * 32, hipMemcpyDeviceToHost, d.stream), "D2H header hashes");
   HKV_TRY(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, d.stream), "D2H header status");
   HKV_TRY(hipStreamSynchronize(d.stream), "headers sync");
-  return HKV_OK;
+  return scratch_release(d, d.stream);
 }
 
 int hkv_merkle_roots_device(hkv_ctx* ctx, int dev, const uint8_t* d_txids, const uint32_t* d_offsets,
@@ -716,7 +787,7 @@ int hkv_merkle_roots_device(hkv_ctx* ctx, int dev, const uint8_t* d_txids, const
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
-  HKV_TRY(hkv::launch_merkle(d_txids, d_offsets, (uint32_t)n_blocks, d_scratch, d_roots, d_mutated, st),
+  HKV_TRY(hkv::launch_merkle(d_txids, d_offsets, (uint32_t)n_blocks, d_scratch, d_roots, d_mutated, (uint32_t)d.n_cu, st),
           "merkle launch");
   return HKV_OK;
 }
@@ -736,8 +807,9 @@ int hkv_merkle_roots(hkv_ctx* ctx, const uint8_t* txids, const uint32_t* offsets
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   // one staging buffer: txids (L*32) | scratch (L*32) | roots (B*32) | offsets ((B+1)*4) | mutated (B)
   const size_t off_bytes = (n_blocks + 1) * 4;
-  int rc = grow(&d.stage[6], &d.stage_cap[6], leaves * 64 + n_blocks * 32 + off_bytes + n_blocks,
-                "hipMalloc(merkle batch)");
+  int rc = scratch_acquire(d, d.stream);
+  if (!rc) rc = grow(&d.stage[6], &d.stage_cap[6], leaves * 64 + n_blocks * 32 + off_bytes + n_blocks,
+                     "hipMalloc(merkle batch)");
   if (rc) return rc;
   uint8_t* b = static_cast<uint8_t*>(d.stage[6]);
   uint8_t *dl = b, *dsc = dl + leaves * 32, *dr = dsc + leaves * 32, *doff = dr + n_blocks * 32,
@@ -745,12 +817,12 @@ int hkv_merkle_roots(hkv_ctx* ctx, const uint8_t* txids, const uint32_t* offsets
   if (leaves) HKV_TRY(hipMemcpyAsync(dl, txids, leaves * 32, hipMemcpyHostToDevice, d.stream), "H2D txids");
   HKV_TRY(hipMemcpyAsync(doff, offsets, off_bytes, hipMemcpyHostToDevice, d.stream), "H2D merkle offsets");
   HKV_TRY(hkv::launch_merkle(dl, reinterpret_cast<const uint32_t*>(doff), (uint32_t)n_blocks, dsc, dr, dm,
-                             d.stream),
+                             (uint32_t)d.n_cu, d.stream),
           "merkle launch");
   HKV_TRY(hipMemcpyAsync(roots_out, dr, n_blocks * 32, hipMemcpyDeviceToHost, d.stream), "D2H merkle roots");
   HKV_TRY(hipMemcpyAsync(mutated, dm, n_blocks, hipMemcpyDeviceToHost, d.stream), "D2H merkle mutated");
   HKV_TRY(hipStreamSynchronize(d.stream), "merkle sync");
-  return HKV_OK;
+  return scratch_release(d, d.stream);
 }
 
 }  // extern "C"

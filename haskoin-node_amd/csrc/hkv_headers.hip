@@ -349,9 +349,9 @@ __global__ void __launch_bounds__(64) hkv_merkle_top_kernel(const uint32_t* __re
 }
 
 hipError_t launch_merkle(const uint8_t* leaves, const uint32_t* offsets, uint32_t n_blocks, uint8_t* scratch,
-                         uint8_t* roots, uint8_t* mutated, hipStream_t st) {
+                         uint8_t* roots, uint8_t* mutated, uint32_t n_cu, hipStream_t st) {
   if (n_blocks == 0) return hipSuccess;
-  if (n_blocks <= 256) {  // fewer blocks than CUs: split each tree over MERKLE_SPLIT workgroups
+  if (n_blocks <= n_cu) {  // no more blocks than CUs: split each tree over MERKLE_SPLIT workgroups
     hipLaunchKernelGGL(hkv_merkle_sub_kernel, dim3(n_blocks * MERKLE_SPLIT), dim3(WG), 0, st,
                        reinterpret_cast<const uint32_t*>(leaves), offsets, reinterpret_cast<uint32_t*>(scratch));
     hipError_t e = hipGetLastError();

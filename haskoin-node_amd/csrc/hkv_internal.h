@@ -28,7 +28,7 @@ namespace hkv {
 hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im,
                            hipStream_t st);
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, bool split, hipStream_t st);
+                         uint32_t grid, uint32_t* bits, bool split, unsigned long long* clk, hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
 hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,
@@ -52,5 +52,5 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
 hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
                           uint8_t* hashes, uint8_t* status, hipStream_t st);
 hipError_t launch_merkle(const uint8_t* leaves, const uint32_t* offsets, uint32_t n_blocks, uint8_t* scratch,
-                         uint8_t* roots, uint8_t* mutated, hipStream_t st);
+                         uint8_t* roots, uint8_t* mutated, uint32_t n_cu, hipStream_t st);
 }  // namespace hkv

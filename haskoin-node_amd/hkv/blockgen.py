@@ -1,8 +1,13 @@
-"""Synthetic mainnet-shaped block mix (BASELINE.json configs[2], SURVEY.md
-§8(d) config 3) for the benchmark and the tests.
+"""Synthetic blocks for the benchmark and the tests.
 
-2,000 txs (default), each spending 1-3 prevouts (60% P2WPKH / 40% P2PKH) and
-paying 2 P2PKH outputs, SIGHASH_ALL, no fork id. Keys, sighashes and
+* ``make_block`` — the mainnet-shaped block mix (BASELINE.json configs[2],
+  SURVEY.md §8(d) config 3): 2,000 txs (default), each spending 1-3 prevouts
+  (60% P2WPKH / 40% P2PKH) and paying 2 P2PKH outputs, SIGHASH_ALL, no fork id.
+* ``make_p2pkh_block`` — the CPU-reference block (BASELINE.json configs[0],
+  SURVEY.md §8(d) config 1): 2,000 txs x 2 P2PKH inputs x 2 P2PKH outputs =
+  4,000 signatures, compressed keys from a pool of 4,096, SIGHASH_ALL, low S,
+  seed 0x484B5631.
+ Keys, sighashes and
 signatures come from libhkv's device hooks (hkv_gen_keys_device,
 hkv_sighash, hkv_gen_sign_device): the sighash of a tx does not depend on its
 scriptSigs / witnesses, so the block is hashed as a skeleton, signed, then
@@ -22,6 +27,7 @@ from .lib import HKV_SIGHASH_FORKID, HKV_SIGHASH_LEGACY
 from .sighash import tx_sig_hash_batch
 
 SEED = 0x484B5633
+P2PKH_SEED = 0x484B5631
 
 
 def varint(n: int) -> bytes:
@@ -71,7 +77,8 @@ def serialize(version, ins, outs, wit, lock) -> bytes:
 
 
 def make_block(verifier, torch, n_tx: int = 2000, seed: int = SEED, n_keys: int = 4096,
-               p2wpkh_share: float = 0.6) -> Tuple[List[bytes], List[Tuple[int, int, bytes, int]]]:
+               p2wpkh_share: float = 0.6, inputs_per_tx=(1, 1, 2, 2, 3)
+               ) -> Tuple[List[bytes], List[Tuple[int, int, bytes, int]]]:
     """Returns (serialised txs, inputs) with inputs = (tx, input index, prevout
     scriptPubKey, prevout value): the arguments of verify_std_inputs."""
     rng = random.Random(seed)
@@ -84,7 +91,7 @@ def make_block(verifier, torch, n_tx: int = 2000, seed: int = SEED, n_keys: int 
 
     txs, meta, jobs, key_idx = [], [], [], []
     for t in range(n_tx):
-        nin = rng.choice([1, 1, 2, 2, 3])
+        nin = rng.choice(inputs_per_tx)
         ins, kinds = [], []
         for j in range(nin):
             k = rng.randrange(n_keys)
@@ -126,6 +133,12 @@ def make_block(verifier, torch, n_tx: int = 2000, seed: int = SEED, n_keys: int 
             q += 1
         out_txs.append(serialize(version, new_ins, outs, wit, lock))
     return out_txs, inputs
+
+
+def make_p2pkh_block(verifier, torch, n_tx: int = 2000, seed: int = P2PKH_SEED
+                     ) -> Tuple[List[bytes], List[Tuple[int, int, bytes, int]]]:
+    """BASELINE configs[0]: n_tx txs x 2 P2PKH inputs x 2 P2PKH outputs."""
+    return make_block(verifier, torch, n_tx=n_tx, seed=seed, n_keys=4096, p2wpkh_share=0.0, inputs_per_tx=(2,))
 
 
 class DeviceBlock:

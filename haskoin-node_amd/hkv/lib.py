@@ -96,6 +96,7 @@ EXPORTS = {
     "hkv_profile_enable": (c_int, [c_void_p, c_int]),
     "hkv_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                  POINTER(c_uint64)]),
+    "hkv_profile_clock": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double)]),
     "hkv_strerror": (c_char_p, [c_int]),
     "hkv_last_hip_error": (c_char_p, []),
     "hkv_device_count": (c_int, []),

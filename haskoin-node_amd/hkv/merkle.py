@@ -3,7 +3,10 @@
 Haskoin.Block.Merkle], which the reference checks against every fetched
 block's header (/root/reference/test/Haskoin/NodeSpec.hs:185-193, blocks from
 ``getBlocks``, src/Haskoin/Node/Peer.hs:309-344). All hashing runs in libhkv's
-HIP kernel (csrc/hkv_headers.hip, hkv_merkle_kernel), one workgroup per block.
+HIP kernels (csrc/hkv_headers.hip), on one of two routes: batches of at most
+n_cu blocks (256 on an MI355X) split each tree over 8 aligned-subtree
+workgroups (hkv_merkle_sub_kernel) joined by hkv_merkle_top_kernel; larger
+batches take one workgroup per block (hkv_merkle_kernel).
 
     merkle_roots(v, blocks) -> (roots: list of 32-byte digests, mutated: bool[n])
 

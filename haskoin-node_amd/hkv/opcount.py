@@ -57,16 +57,45 @@ def prologue_products() -> int:
     return sqrt + curve + inv_per_sig + 2 * SC_MUL + glv
 
 
+# --- the reference algorithm's work (the frozen roofline numerator) ---------
+# P_alg is counted for the REFERENCE algorithm, not for this
+# implementation, so it does not drift when the kernels change. libsecp256k1's
+# secp256k1_ecmult for one point [dep; published algorithm]: GLV split of u2,
+# wNAF w = 5 over both 129-bit halves (expected density 1/(w+1)), the 8-entry
+# odd-multiples table of Q on a global Z (secp256k1_ecmult_odd_multiples_table
+# + secp256k1_ge_table_set_globalz) plus its lambda image (beta * x), G and
+# 2^128 G by precomputed w = 15 tables (ECMULT_WINDOW_SIZE default) added with
+# secp256k1_gej_add_zinv_var, 129 doublings (secp256k1_gej_double: 3M + 4S),
+# then the Jacobian x compare (1S + 1M). Field products are priced at this
+# ISA's 32-bit limb-product counts (FE_MUL / FE_SQR above).
+REF_BITS = 129                      # |k1|, |k2| < 2^129 after the GLV split
+REF_WNAF_Q = 5
+REF_WINDOW_G = 15
+REF_Q_ADDS = 2 * REF_BITS / (REF_WNAF_Q + 1)     # 43
+REF_G_ADDS = 2 * 128 / (REF_WINDOW_G + 1)        # 16
+REF_TABLE = ((3 * FE_MUL + 4 * FE_SQR)            # 2Q
+             + 7 * (8 * FE_MUL + 3 * FE_SQR)      # 3Q .. 15Q (odd multiples, mixed adds)
+             + 7 * (4 * FE_MUL + FE_SQR)          # global-Z rescale
+             + 8 * FE_MUL)                        # lambda table: beta * x
+REF_LADDER = (REF_BITS * (3 * FE_MUL + 4 * FE_SQR) + REF_Q_ADDS * (8 * FE_MUL + 3 * FE_SQR)
+              + REF_G_ADDS * (9 * FE_MUL + 3 * FE_SQR))
+REF_COMPARE = FE_SQR + FE_MUL
+P_ALG_ECMULT = int(round(REF_TABLE + REF_LADDER + REF_COMPARE))
+
 ECMULT_PRODUCTS_PER_VERIFY = ecmult_products()
 PROLOGUE_PRODUCTS_PER_VERIFY = prologue_products()
 PRODUCTS_PER_VERIFY = ECMULT_PRODUCTS_PER_VERIFY + PROLOGUE_PRODUCTS_PER_VERIFY
 
-# measured v_mad_u64_u32 issue rate on gfx950 (lane-products / clk / CU)
+# v_mad_u64_u32 issue rate on gfx950 (lane-products / clk / CU): nominal half
+# rate (64), and the rate measured by tools/ubench_int.hip
+# (profiles/r01_ubench_int.json: 57.07 at the clock it ran at)
 R_MUL = 64
+R_MUL_MEASURED = 57.07
 N_CU = 256
 F_CLK_PEAK = 2.4e9
 PEAK_PRODUCTS_PER_S = R_MUL * N_CU * F_CLK_PEAK
 
 if __name__ == "__main__":
+    print("P_alg(ecmult, reference algorithm)", P_ALG_ECMULT, "P_impl(ecmult)", ECMULT_PRODUCTS_PER_VERIFY)
     print("ecmult", ECMULT_PRODUCTS_PER_VERIFY, "prologue", PROLOGUE_PRODUCTS_PER_VERIFY,
           "total", PRODUCTS_PER_VERIFY, "peak/s %.3e" % PEAK_PRODUCTS_PER_S)

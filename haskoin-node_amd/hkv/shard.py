@@ -1,10 +1,15 @@
 """Signature-index sharding across GPUs: contiguous ranges,
 64-aligned starts (a wave's ballot word pair never straddles two ranks), the
 remainder on the last rank. The same rule as hkv_api.cpp's in-process
-sharding, so a 1-GPU and an N-GPU run produce bit-identical bitmaps."""
+sharding, so a 1-GPU and an N-GPU run produce bit-identical bitmaps.
+
+``ShardedVerify`` is one rank's step of the one-process-per-GPU run that
+bench.py times: verify the rank's shard into its verdict words, then ONE
+all-gather of every rank's words (RCCL over xGMI on the GPU box; the only
+collective on the path), then ``bitmap()`` assembles the global bitmap."""
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Callable, Tuple
 
 import numpy as np
 
@@ -19,6 +24,13 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, hi
 
 
+def words_per_rank(n: int, world: int) -> int:
+    """uint32 words in each rank's all-gather slot: the largest shard's
+    ballot words (two per 64 signatures) plus two spare."""
+    longest = max(hi - lo for lo, hi in (shard_bounds(n, r, world) for r in range(world)))
+    return (longest + 63) // 64 * 2 + 2
+
+
 def assemble_bitmap(n: int, world: int, gathered_words: np.ndarray, words_per_rank: int) -> np.ndarray:
     """gathered_words: [world * words_per_rank] uint32 from an all-gather of
     each rank's shard bitmap (rank r's bits start at bit 0 of its slot).
@@ -31,3 +43,37 @@ def assemble_bitmap(n: int, world: int, gathered_words: np.ndarray, words_per_ra
         w = (hi - lo + 31) // 32
         out[lo // 32: lo // 32 + w] |= gathered_words[r * words_per_rank: r * words_per_rank + w]
     return out
+
+
+class ShardedVerify:
+    """One rank's verify step over its shard of an n-signature batch.
+
+    verify: called as verify(lo, hi, bits) — must write the verdict words of
+    records [lo, hi) into the int32 tensor ``bits`` (hkv_verify_device on the
+    rank's GPU in bench.py; a CPU checker in the gloo tests).
+    dist: torch.distributed (None or world == 1: no collective)."""
+
+    def __init__(self, torch, n: int, rank: int, world: int, verify: Callable, dist=None, device: str = "cuda"):
+        self.n, self.rank, self.world = n, rank, world
+        self.lo, self.hi = shard_bounds(n, rank, world)
+        self.wpr = words_per_rank(n, world)
+        self.verify = verify
+        self.dist = dist if world > 1 else None
+        self.bits = torch.zeros(self.wpr, dtype=torch.int32, device=device)
+        self.gathered = torch.zeros(self.wpr * world, dtype=torch.int32, device=device) if self.dist else None
+
+    @property
+    def local_n(self) -> int:
+        return self.hi - self.lo
+
+    def step(self) -> None:
+        """Verify the shard, then the one all-gather of the verdict words."""
+        self.verify(self.lo, self.hi, self.bits)
+        if self.dist is not None:
+            self.dist.all_gather_into_tensor(self.gathered, self.bits)
+
+    def bitmap(self) -> np.ndarray:
+        """The global verdict bitmap (ceil(n/32) words) after step()."""
+        if self.dist is None:
+            return self.bits.cpu().numpy().view(np.uint32)[: (self.n + 31) // 32].copy()
+        return assemble_bitmap(self.n, self.world, self.gathered.cpu().numpy().view(np.uint32), self.wpr)

@@ -36,6 +36,10 @@
  *       from importHeaders (/root/reference/src/Haskoin/Node/Chain.hs:500-520):
  *       headerHash, isValidPOW (decodeCompact) and the prev-hash link.
  *
+ * Streams: device-form calls enqueue on the caller's stream; calls on one
+ * device share its scratch buffers, so each call is ordered after the
+ * previous call on that device (an event wait), whatever stream either used.
+ *
  * Conventions: no C++ exceptions cross this boundary; every function that
  * can fail returns 0 (HKV_OK) or a negative hkv_err. A verdict is never an
  * error: malformed records simply get bit 0. Verdict bit i of the output is
@@ -268,6 +272,10 @@ int hkv_debug_op(hkv_ctx* ctx, int dev, uint32_t op, size_t n, const uint32_t* d
  * read: synchronises, returns summed milliseconds and the launch count, resets. */
 int hkv_profile_enable(hkv_ctx* ctx, int on);
 int hkv_profile_read(hkv_ctx* ctx, int dev, double* prologue_ms, double* ecmult_ms, uint64_t* launches);
+/* Shader clock (MHz) block 0 of the last profiled ecmult launch ran at:
+ * clock64() / wall_clock64() deltas around its work (so the roofline can be
+ * priced at the measured clock). Synchronises the device. */
+int hkv_profile_clock(hkv_ctx* ctx, int dev, double* sclk_mhz);
 
 const char* hkv_strerror(int err);
 const char* hkv_last_hip_error(void);

@@ -46,6 +46,47 @@ def coracle():
     return lib
 
 
+OPENSSL_SO = os.path.join(ROOT, "oracle", "build", "libhkv_openssl.so")
+
+
+@pytest.fixture(scope="session")
+def openssl():
+    """OpenSSL 3 ECDSA_do_verify behind the semantic adapter
+    (oracle/openssl_check.c): an implementation-independent checker."""
+    import ctypes
+    if not os.path.exists(OPENSSL_SO):
+        import subprocess
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                       stdout=subprocess.DEVNULL)
+    lib = ctypes.CDLL(OPENSSL_SO)
+    lib.hkvo_openssl_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_int]
+    lib.hkvo_openssl_verify_batch.restype = ctypes.c_int
+    return lib
+
+
+def openssl_batch(lib, recs_bytes: bytes, mode: int, threads: int = 8):
+    import ctypes
+    import numpy as np
+    n = len(recs_bytes) // 168
+    out = np.zeros(n, dtype=np.uint8)
+    buf = np.frombuffer(recs_bytes, dtype=np.uint8)
+    rc = lib.hkvo_openssl_verify_batch(buf.ctypes.data_as(ctypes.c_void_p), n, mode,
+                                       out.ctypes.data_as(ctypes.c_void_p), threads)
+    assert rc == 0, "OpenSSL could not build a secp256k1 key"
+    return out.astype(bool)
+
+
+def host_threads() -> int:
+    """Worker threads for the CPU checkers: this process's CPU share (the GPU
+    box gives a job 16 CPUs even where os.cpu_count() shows the whole host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+
+
 def oracle_batch(lib, recs_bytes: bytes, mode: int, threads: int = 8):
     import ctypes
     import numpy as np

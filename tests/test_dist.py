@@ -22,45 +22,48 @@ def _free_port():
 
 
 def _worker(rank, world, port, n, q):
+    """One rank of the bench's multi-GPU step (hkv.shard.ShardedVerify: shard
+    verify + the one all-gather + bitmap assembly), with the C oracle as the
+    CPU stand-in for hkv_verify_device."""
     import ctypes
     import sys
     import torch
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(here, "..", "haskoin-node_amd"))
     from hkv.records import bits_from_bools
-    from hkv.shard import assemble_bitmap, shard_bounds
+    from hkv.shard import ShardedVerify
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     data = open(os.path.join(GOLDEN, "kat_records.bin"), "rb").read()
     m = len(data) // 168
     recs = b"".join(data[(i % m) * 168:(i % m + 1) * 168] for i in range(n))
-    lo, hi = shard_bounds(n, rank, world)
     lib = ctypes.CDLL(ORACLE_SO)
-    out = np.zeros(hi - lo, dtype=np.uint8)
-    buf = np.frombuffer(recs[lo * 168:hi * 168], dtype=np.uint8)
-    lib.hkvo_verify_batch(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(hi - lo), 1,
-                          ctypes.c_void_p(out.ctypes.data), 2)
-    wpr = (-(-n // world) + 63) // 64 * 2 + 2
-    mine = np.zeros(wpr, dtype=np.uint32)
-    w = bits_from_bools(out.astype(bool))
-    mine[: len(w)] = w
-    t = torch.from_numpy(mine.view(np.int32))
-    gathered = torch.zeros(wpr * world, dtype=torch.int32)
-    dist.all_gather_into_tensor(gathered, t)
-    full = assemble_bitmap(n, world, gathered.numpy().view(np.uint32), wpr)
+
+    def cpu_verify(lo, hi, bits):
+        out = np.zeros(hi - lo, dtype=np.uint8)
+        buf = np.frombuffer(recs[lo * 168:hi * 168], dtype=np.uint8)
+        lib.hkvo_verify_batch(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(hi - lo), 1,
+                              ctypes.c_void_p(out.ctypes.data), 2)
+        w = bits_from_bools(out.astype(bool))
+        bits.zero_()
+        bits[: len(w)] = torch.from_numpy(w.view(np.int32))
+
+    sv = ShardedVerify(torch, n, rank, world, cpu_verify, dist=dist, device="cpu")
+    sv.step()
+    full = sv.bitmap()
     if rank == 0:
         q.put(full.tobytes())
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [1000, 64 * 7 + 5])
-def test_two_rank_bitmap_equals_single(n, coracle):
+@pytest.mark.parametrize("n,world", [(1000, 2), (64 * 7 + 5, 2), (3 * 64 + 1, 3)])
+def test_two_rank_bitmap_equals_single(n, world, coracle):
     import ctypes
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = np.frombuffer(q.get(timeout=120), dtype=np.uint32)

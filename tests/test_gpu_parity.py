@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import secp256k1_oracle as o
-from conftest import oracle_batch
+from conftest import host_threads, openssl_batch, oracle_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -185,22 +185,15 @@ def gen_device(torch, ver, n, seed, unc=100, pool=65536):
     return d
 
 
-def adversarial(host: np.ndarray, seed: int) -> np.ndarray:
-    """Mutate ~30% of valid records into SURVEY §8(c) invalid classes (config 4)."""
-    rng = np.random.default_rng(seed)
-    a = host.reshape(-1, 168).copy()
-    n = a.shape[0]
-    cls = rng.integers(0, 20, size=n)  # 0..5 -> mutated (30%)
-    idx = np.nonzero(cls == 0)[0]; a[idx, rng.integers(0, 32, len(idx))] ^= 1            # msg bit
-    idx = np.nonzero(cls == 1)[0]; a[idx, 32:64] = 0                                      # r = 0
-    idx = np.nonzero(cls == 2)[0]; a[idx, 64:96] = 0xFF                                   # s >= n
-    idx = np.nonzero(cls == 3)[0]; a[idx, 97] ^= 0x04                                     # bad prefix
-    idx = np.nonzero(cls == 4)[0]; a[idx, 98:130] = 0xFF                                  # x >= p
-    idx = np.nonzero(cls == 5)[0]                                                         # high-S
-    for i in idx:
-        s = int.from_bytes(a[i, 64:96].tobytes(), "big")
-        a[i, 64:96] = np.frombuffer((o.N - s).to_bytes(32, "big"), dtype=np.uint8)
-    return a.reshape(-1)
+def gen_twin(torch, ver, d, n, seed):
+    """The same generated records with every key in 65-byte form (same seed,
+    uncompressed_permille = 1000): the y source of hkv.adversarial.mutate."""
+    t = gen_device(torch, ver, n, seed=seed, unc=1000).cpu().numpy()
+    a, b = d.cpu().numpy().reshape(-1, 168), t.reshape(-1, 168)
+    assert (a[:, :96] == b[:, :96]).all() and (a[:, 98:130] == b[:, 98:130]).all()
+    comp = a[:, 96] == 33
+    assert ((a[comp, 97] & 1) == (b[comp, 161] & 1)).all()  # prefix parity == y parity
+    return t
 
 
 def test_generated_valid_batch_all_accept_and_oracle_agrees(torch, ver, coracle):
@@ -214,16 +207,22 @@ def test_generated_valid_batch_all_accept_and_oracle_agrees(torch, ver, coracle)
     assert exp.all()
 
 
-def test_adversarial_batch_vs_oracle(torch, ver, coracle):
+def test_adversarial_batch_vs_oracle(torch, ver, coracle, openssl):
+    """131,072 records, 30% invalid over every hkv.adversarial class (plus 5%
+    special valids): GPU == C restatement == OpenSSL, both modes."""
+    from hkv import adversarial
     n = 131072
     d = gen_device(torch, ver, n, seed=0x484B5634, unc=100)
-    adv = adversarial(d.cpu().numpy(), 11)
-    for mode in (0, 1):
-        exp = oracle_batch(coracle, adv.tobytes(), mode, threads=16)
+    twin = gen_twin(torch, ver, d, n, 0x484B5634)
+    adv, lab_lib, lab_hask, cls = adversarial.mutate(d.cpu().numpy(), seed=11, twin=twin)
+    for mode, lab in ((0, lab_lib), (1, lab_hask)):
+        exp = oracle_batch(coracle, adv.tobytes(), mode, threads=host_threads())
         got = ver.verify_records(adv, mode)
         mism = np.nonzero(got != exp)[0]
-        assert mism.size == 0, (mode, mism[:20])
-        assert 0.6 < exp.mean() < 0.8
+        assert mism.size == 0, (mode, mism[:20], [adversarial.CLASSES[c] for c in cls[mism[:20]]])
+        assert (exp == lab).all()
+        sl = slice(0, 16384 * 168)
+        assert (openssl_batch(openssl, adv[sl].tobytes(), mode, threads=host_threads()) == got[:16384]).all()
 
 
 def test_device_path_and_determinism(torch, ver):
@@ -274,24 +273,35 @@ def verify_dev_bits(torch, ver, d, n, mode, offset=0):
     return words.cpu().numpy().view(np.uint32)
 
 
-def test_config4_adversarial_1m_both_modes(torch, ver, coracle):
-    """BASELINE configs[3]: 1,048,576 records, 30% invalid over the §8(c)
-    classes, exact reject parity in both modes against the construction labels
-    (hkv/adversarial.py, pinned per class by test_adversarial_labels.py) and a
-    32k slice against the C oracle."""
+def test_config4_adversarial_1m_both_modes(torch, ver, coracle, openssl):
+    """BASELINE configs[3]: 1,048,576 records, 30% invalid spread evenly over
+    every SURVEY §8(c) class hkv.adversarial builds (msg bit, r/s in {0, n,
+    n+k, 2^256-1}, bad / flipped prefixes, x >= p, y >= p, off-curve,
+    non-residue x, hybrid parity, 33/65 length mismatch, wrong Q, sum = inf,
+    r = R.x >= n, high-S) plus 5% special valids (re-encoded and hybrid keys,
+    the r + n branch, edge u1 / u2, u1 = 0, msg32 >= n, ladder collisions).
+    The GPU bitmap must equal, in both modes and on EVERY record, the
+    construction labels and the C restatement; a 262,144-record slice must
+    also equal OpenSSL's ECDSA_do_verify behind the semantic adapter."""
     from hkv import adversarial
     n = 1 << 20
     d = gen_device(torch, ver, n, seed=0x484B5634)
-    adv, lab_lib, lab_hask, cls = adversarial.mutate(d.cpu().numpy(), seed=0x484B5634)
-    assert 0.29 < (cls >= 0).mean() < 0.31
+    twin = gen_twin(torch, ver, d, n, 0x484B5634)
+    adv, lab_lib, lab_hask, cls = adversarial.mutate(d.cpu().numpy(), seed=0x484B5634, twin=twin)
+    assert 0.29 < np.isin(cls, np.arange(len(adversarial.INVALID_CLASSES))).mean() < 0.31
     d.copy_(torch.from_numpy(adv))
+    th = host_threads()
     for mode, lab in ((0, lab_lib), (1, lab_hask)):
         got = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n, mode), n)
         mism = np.nonzero(got != lab)[0]
-        assert mism.size == 0, (mode, mism[:10], cls[mism[:10]])
-        sl = slice(500_000 * 168, (500_000 + 32768) * 168)
-        exp = oracle_batch(coracle, adv[sl].tobytes(), mode, threads=16)
-        assert (got[500_000:500_000 + 32768] == exp).all()
+        assert mism.size == 0, (mode, mism[:10], [adversarial.CLASSES[c] for c in cls[mism[:10]]])
+        exp = oracle_batch(coracle, adv.tobytes(), mode, threads=th)
+        mism = np.nonzero(got != exp)[0]
+        assert mism.size == 0, (mode, "C oracle", mism[:10])
+        lo = 400_000
+        sl = slice(lo * 168, (lo + 262144) * 168)
+        ossl = openssl_batch(openssl, adv[sl].tobytes(), mode, threads=th)
+        assert (got[lo:lo + 262144] == ossl).all(), (mode, "openssl")
 
 
 def test_config5_ibd_16m_sharded_bitmap(torch, ver):
@@ -303,7 +313,10 @@ def test_config5_ibd_16m_sharded_bitmap(torch, ver):
     from hkv.shard import assemble_bitmap, shard_bounds
     n, world = 1 << 24, 8
     d = gen_device(torch, ver, n, seed=0x484B5635)
-    adv, lab, _, _ = adversarial.mutate(d.cpu().numpy(), seed=0x484B5635, invalid_frac=0.05)
+    twin = gen_twin(torch, ver, d, n, 0x484B5635)
+    adv, lab, _, _ = adversarial.mutate(d.cpu().numpy(), seed=0x484B5635, invalid_frac=0.05, special_frac=0.0,
+                                        twin=twin)
+    del twin
     d.copy_(torch.from_numpy(adv))
     del adv
     whole = verify_dev_bits(torch, ver, d, n, 0)[: (n + 31) // 32]
@@ -361,3 +374,53 @@ def test_host_path_pipelined_chunks_match_device_path(torch, ver):
 def adversarial_unpack(words, n):
     from hkv import adversarial
     return adversarial.unpack_bits(words, n)
+
+
+def test_two_device_contexts_on_one_gpu_match_single(torch, ver):
+    """hkv_open_devices([0, 0]): the in-process multi-device path of
+    hkv_verify (hkv_api.cpp verify_from_host: contiguous 64-aligned shards,
+    per-device copy / verify streams, H2D pipelined in grid-sized chunks, the
+    per-shard verdict words merged into the caller's bitmap) exercised with
+    two device contexts on one GPU. n = 5 * 2^18 + 17 gives each shard three
+    chunks (262,144 + 262,144 + 131,136 / + 131,153) and a ragged last word;
+    2% of the records are corrupted."""
+    import hkv
+    n = 5 * (1 << 18) + 17
+    d = gen_device(torch, ver, n, seed=0x4D554C54)
+    host = d.cpu().numpy().copy()
+    rng = np.random.default_rng(12)
+    bad = rng.choice(n, size=n // 50, replace=False)
+    host[bad * 168 + 40] ^= 0x01                       # a bit of r: ECDSA rejects
+    single = ver.verify_records(host, 0)
+    with hkv.Verifier(hkv.VerifierConfig(device_ids=[0, 0], flags=1)) as v2:
+        assert v2.num_devices == 2
+        for mode in (0, 1):
+            got = v2.verify_records(host, mode)
+            assert (got == single).all(), np.nonzero(got != single)[0][:10]
+    assert not single[bad].any() and single.sum() == n - bad.size
+
+
+def test_scratch_ordered_across_streams(torch, ver):
+    """Device-form calls on two different streams share the device's scratch
+    (intermediate, Q tables, verdict words): each call waits for the previous
+    call's work (include/hkv.h, Streams), so back-to-back verifies of two
+    different batches on two streams each get their own verdicts."""
+    n = 200_000
+    a = gen_device(torch, ver, n, seed=0x53545231)
+    b = a.clone()
+    b.view(-1, 168)[::3, 5] ^= 0x20                   # every third record of b rejects
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    wa = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    wb = torch.zeros_like(wa)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        ver.verify_device(0, a.data_ptr(), n, 0, wa.data_ptr(), s1.cuda_stream)
+        ver.verify_device(0, b.data_ptr(), n, 0, wb.data_ptr(), s2.cuda_stream)
+    torch.cuda.synchronize()
+    from hkv import adversarial
+    ga = adversarial.unpack_bits(wa.cpu().numpy().view(np.uint32), n)
+    gb = adversarial.unpack_bits(wb.cpu().numpy().view(np.uint32), n)
+    assert ga.all()
+    exp = np.ones(n, dtype=bool)
+    exp[::3] = False
+    assert (gb == exp).all()

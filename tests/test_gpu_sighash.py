@@ -13,7 +13,7 @@ import pytest
 import secp256k1_oracle as o
 import sighash_oracle as sh
 import txgen
-from conftest import GOLDEN, oracle_batch
+from conftest import host_threads, openssl_batch, GOLDEN, oracle_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -264,17 +264,53 @@ def test_gen_keys_and_sign(torch, ver, coracle):
     assert oracle_batch(coracle, b"".join(recs), 0).all()
 
 
-def test_block_mix_config3_all_valid(torch, ver, coracle):
-    """BASELINE configs[2]: 2,000-tx P2PKH + P2WPKH block from the product-side
-    generator verifies end to end; a sample is re-derived by the oracle."""
+def _block_vs_oracle(torch, ver, coracle, openssl, txs, inputs):
+    """Every input's 168-byte verify record (msg32 = the sighash, r, s, key)
+    equals the oracle's std_input_record (Python txSigHash / decodeTxSig /
+    HASH160 restatement); verdicts equal the C restatement and OpenSSL."""
     import hkv
+    got = hkv.verify_std_inputs(ver, txs, inputs)
+    recs = device_std_records(torch, ver, txs, inputs, None)
+    parsed = [sh.tx_parse(t) for t in txs]
+    exp = b"".join(sh.std_input_record(parsed[t], i, p, v) for (t, i, p, v) in inputs)
+    bad = [k for k in range(len(inputs)) if recs[k * 168:(k + 1) * 168] != exp[k * 168:(k + 1) * 168]]
+    assert not bad, bad[:10]
+    assert got == oracle_batch(coracle, exp, 1, threads=host_threads()).tolist()
+    assert got == openssl_batch(openssl, exp, 1, threads=host_threads()).tolist()
+    return got
+
+
+def test_block_mix_config3_all_valid(torch, ver, coracle, openssl):
+    """BASELINE configs[2]: 2,000-tx P2PKH + P2WPKH block from the product-side
+    generator verifies end to end; EVERY input's record is re-derived by the
+    oracle (so a sighash bug shared by signer and verifier cannot hide)."""
     from hkv import blockgen
     txs, inputs = blockgen.make_block(ver, torch, n_tx=2000)
     assert 3000 < len(inputs) < 5000
-    got = hkv.verify_std_inputs(ver, txs, inputs)
-    assert all(got)
-    sample = inputs[::37]
-    recs = device_std_records(torch, ver, txs, sample, None)
-    exp = b"".join(sh.std_input_record(sh.tx_parse(txs[t]), i, p, v) for (t, i, p, v) in sample)
-    assert recs == exp
-    assert oracle_batch(coracle, exp, 1).all()
+    assert all(_block_vs_oracle(torch, ver, coracle, openssl, txs, inputs))
+
+
+def test_p2pkh_block_config0(torch, ver, coracle, openssl):
+    """BASELINE configs[0]: 2,000 txs x 2 P2PKH inputs x 2 P2PKH outputs =
+    4,000 signatures (seed 0x484B5631, 4,096-key pool, compressed keys,
+    SIGHASH_ALL): every record byte-exact against the oracle, every verdict
+    accepted and equal to both CPU checkers; one mutated input per tx
+    (a flipped scriptSig signature byte) rejects exactly those inputs."""
+    from hkv import blockgen
+    txs, inputs = blockgen.make_p2pkh_block(ver, torch)
+    assert len(txs) == 2000 and len(inputs) == 4000
+    assert all(len(p) == 25 for (_, _, p, _) in inputs)
+    assert all(_block_vs_oracle(torch, ver, coracle, openssl, txs, inputs))
+    rng = random.Random(0x484B5631)
+    bad_txs, flips = [], []
+    for t, raw in enumerate(txs):
+        tx = sh.tx_parse(raw)
+        i = rng.randrange(2)
+        items = sh._push_items(tx.inputs[i].script)
+        sig = items[0]
+        sig = sig[:7] + bytes([sig[7] ^ 0x10]) + sig[8:]  # a byte of r: ECDSA (or DER) must reject
+        tx.inputs[i].script = txgen.push(sig) + txgen.push(items[1])
+        bad_txs.append(sh.tx_serialize(tx))
+        flips.append(2 * t + i)
+    got = _block_vs_oracle(torch, ver, coracle, openssl, bad_txs, inputs)
+    assert [k for k, v in enumerate(got) if not v] == flips

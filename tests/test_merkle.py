@@ -107,27 +107,41 @@ def test_gpu_known_answers(verifier):
     assert not mut.any()
 
 
+def _edge_blocks(seed):
+    """EDGE_SIZES with level-0 duplicates (dup_frac), an inner-level duplicate
+    (6 leaves, level-1 pair equal) and top-join-only duplicates: 16 leaves
+    whose second half repeats the first (equal subtree roots; with 8 subtree
+    workgroups only hkv_merkle_top_kernel pairs them) and 4,096 leaves with
+    the upper 2,048 repeating the lower."""
+    rng = random.Random(seed)
+    blocks = random_blocks(EDGE_SIZES, seed=seed, dup_frac=0.5)
+    t = [rng.randbytes(32) for _ in range(6)]
+    t[2], t[3] = t[0], t[1]
+    blocks.append(t)
+    for n in (16, 4096):
+        h = [rng.randbytes(32) for _ in range(n // 2)]
+        blocks.append(h + h)
+    return blocks
+
+
 @pytest.mark.gpu
-def test_gpu_edge_sizes_parity(verifier):
+@pytest.mark.parametrize("route", ["split", "full"])
+def test_gpu_edge_sizes_parity_both_routes(verifier, route):
+    """Batches of at most n_cu (256) blocks take the split route (8 subtree
+    workgroups per block + hkv_merkle_top_kernel); larger ones one workgroup
+    per block (hkv_merkle_kernel). The same edge blocks go through both: as
+    they are (split), and padded with 300 random blocks past the threshold
+    (full)."""
     import hkv
-    blocks = random_blocks(EDGE_SIZES, seed=0x4D524B4C, dup_frac=0.5)
-    roots, mut = hkv.merkle_roots(verifier, blocks)
+    blocks = _edge_blocks(0x4D524B4C)
+    pad = random_blocks([1 + k % 9 for k in range(300)], seed=3) if route == "full" else []
+    roots, mut = hkv.merkle_roots(verifier, pad + blocks)
+    roots, mut = roots[len(pad):], mut[len(pad):]
     for b, t in enumerate(blocks):
         er, em = mo.merkle_root(t)
-        assert roots[b] == er, (b, len(t))
-        assert bool(mut[b]) == em, (b, len(t))
-
-
-@pytest.mark.gpu
-def test_gpu_mutation_at_inner_level(verifier):
-    import hkv
-    rng = random.Random(9)
-    t = [rng.randbytes(32) for _ in range(6)]
-    # 6 leaves: level 1 has 3 nodes; repeating leaves 0..1 as 2..3 pairs two equal level-1 nodes
-    t[2], t[3] = t[0], t[1]
-    roots, mut = hkv.merkle_roots(verifier, [t])
-    er, em = mo.merkle_root(t)
-    assert em and mut[0] and roots[0] == er
+        assert roots[b] == er, (route, b, len(t))
+        assert bool(mut[b]) == em, (route, b, len(t))
+    assert mut[-1] and mut[-2] and mut[-3]
 
 
 @pytest.mark.gpu

@@ -226,3 +226,16 @@ def test_golden_cross_check_openssl(kat):
             if openssl_verdict(c, rec, mode) != m[key]:
                 bad.append((m["class"], key))
     assert not bad, bad
+
+
+def test_golden_all_classes_openssl_adapter(kat, openssl):
+    """The C OpenSSL checker (oracle/openssl_check.c: length / prefix gate
+    before EC_POINT_oct2point, high-S adapter, <= 0 is reject) agrees with
+    the manifest on EVERY golden class, the parser-only ones included."""
+    from conftest import openssl_batch
+    recs, meta = kat
+    data = b"".join(recs)
+    for mode, key in ((0, "libsecp"), (1, "haskoin")):
+        got = openssl_batch(openssl, data, mode)
+        bad = [meta[i]["class"] for i in range(len(meta)) if bool(got[i]) != meta[i][key]]
+        assert not bad, (key, bad)
