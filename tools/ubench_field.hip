@@ -3,15 +3,49 @@
 // fills every SIMD with WAVES waves. Reports SIMD-cycles per wave-op, to set
 // against the primitive's VALU instruction count (the issue-bound floor).
 //
+// Ops 7-10 are the representation study (results in
+// profiles/r02_ubench_field*.json and DESIGN.md §4): a 9 x 29-bit limb field
+// (tools/fe29_proto.h: carry-free v_mad_u64_u32 columns) and a lower bound
+// for 52-bit limbs on v_fma_f64 (only the 5 x 5 product with the exact
+// hi/lo split and integer column accumulation — no normalisation, no
+// reduction), each against the 8 x 32-bit fe_mul / fe_sqr of the product.
+//
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/ubench_field.hip -o tools/ubench_field
+//        (-DHKV_MUL_ASM=0: the row-wise C product instead of the asm scanner)
 #include <cstdio>
 #include <vector>
 #include "../haskoin-node_amd/csrc/hkv_group.h"
+#include "fe29_proto.h"
 
 using namespace hkv;
 constexpr int ITERS = 256;
 
 struct Stamp { unsigned long long t0, t1, r0, r1; };
+
+// 52-bit limbs as doubles: a_i * b_j = hi + lo exactly with
+// hi = fma(a, b, C) - C (C = 1.5 * 2^104: rounds to a multiple of 2^52) and
+// lo = fma(a, b, -hi); both parts go to 64-bit integer column accumulators
+// through their bit patterns (the exponent bias subtracted once per column).
+__device__ __forceinline__ void fp52_mul_lower_bound(double r[5], const double a[5], const double b[5]) {
+  const double C = 0x1.8p104, C2 = 0x1.8p52;
+  uint64_t col[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) col[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const double h = __builtin_fma(a[i], b[j], C);
+      const double l = __builtin_fma(a[i], b[j], C - h) + C2;
+      col[i + j + 1] += (uint64_t)__double_as_longlong(h);
+      col[i + j] += (uint64_t)__double_as_longlong(l);
+    }
+  // the result must go back to doubles for the next multiply
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    r[k] = __longlong_as_double((long long)((col[k] & 0xFFFFFFFFFFFFFull) | 0x4330000000000000ull)) - 0x1p52 +
+           (double)(col[k + 5] & 0xFFFFF);
+}
 
 template <int OP>
 __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, Stamp* st) {
@@ -44,6 +78,32 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, S
     } else if constexpr (OP == 6) {
       bool hz, rz;
       gej_add_ge_core(p, p, p.z, b, p.y, hz, rz, nullptr);
+    } else if constexpr (OP == 7 || OP == 8 || OP == 9) {
+      fe29::fe a29, b29;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { a29.v[k] = p.x.v[k] & fe29::M29; b29.v[k] = b.v[k] & fe29::M29; }
+      a29.v[8] = p.x.v[0] >> 8;
+      b29.v[8] = b.v[1] >> 8;
+      if constexpr (OP == 7) {
+        fe29::mul(a29, a29, b29);
+      } else if constexpr (OP == 8) {
+        fe29::sqr(a29, a29);
+      } else {
+        fe29::sub(a29, a29, b29);
+        fe29::carry(a29);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p.x.v[k] = a29.v[k] ^ a29.v[8];
+    } else if constexpr (OP == 10) {
+      double a52[5], b52[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        a52[k] = (double)(((uint64_t)(p.x.v[k] & 0xFFFFF) << 32) | p.x.v[k + 1]);
+        b52[k] = (double)(((uint64_t)(b.v[k] & 0xFFFFF) << 32) | b.v[k + 1]);
+      }
+      fp52_mul_lower_bound(a52, a52, b52);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) p.x.v[k] = (uint32_t)__double_as_longlong(a52[k]);
     }
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -56,7 +116,8 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, S
 }
 
 static const char* NAMES[] = {"fe_mul", "fe_sqr", "fe_mul x2 (independent)", "fe_add", "fe_sub", "gej_double",
-                              "gej_add_ge (mixed)"};
+                              "gej_add_ge (mixed)", "fe29_mul", "fe29_sqr", "fe29_sub+carry",
+                              "fp52_mul (product only, lower bound)"};
 
 template <int OP>
 void run(int n_cu, int blocks_per_cu) {
@@ -104,6 +165,7 @@ int main() {
   for (int bpc : {1, 2, 4}) {
     run<0>(n_cu, bpc); run<1>(n_cu, bpc); run<2>(n_cu, bpc); run<3>(n_cu, bpc);
     run<4>(n_cu, bpc); run<5>(n_cu, bpc); run<6>(n_cu, bpc);
+    run<7>(n_cu, bpc); run<8>(n_cu, bpc); run<9>(n_cu, bpc); run<10>(n_cu, bpc);
   }
   return 0;
 }
