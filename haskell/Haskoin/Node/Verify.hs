@@ -1,0 +1,271 @@
+{-# LANGUAGE DuplicateRecordFields #-}
+{-# LANGUAGE FlexibleContexts #-}
+{-# LANGUAGE OverloadedRecordDot #-}
+{-# LANGUAGE OverloadedStrings #-}
+{-# LANGUAGE TemplateHaskell #-}
+
+-- | Batch signature verification on MI355X GPUs for a haskoin-node based
+-- validator: the drop-in for per-input 'verifyHashSig' (haskoin-core-1.1.0,
+-- /root/reference/stack.yaml:10) and 'verifyStdInput'.
+--
+-- UNCOMPILED in this repository's image (GHC, stack and cabal are absent;
+-- SURVEY.md §8(c)). It is written against include/hkv.h and the reference's
+-- own idioms, and its byte layout is the one haskoin-node_amd/hkv/records.py
+-- (ctypes) implements and tests/test_host.py checks:
+--
+--   * config record in the style of NodeConfig (src/Haskoin/Node.hs:74-96);
+--   * an actor in the style of withChain (src/Haskoin/Node/Chain.hs:277-307):
+--     a mailbox, a forever/receive loop under withAsync + link;
+--   * fed by the node's events: blocks and txs arrive as
+--     PeerEvent (PeerMessage p (MBlock b)) / (MTx t), which
+--     Haskoin.Node.peerEvents (src/Haskoin/Node.hs:151-174) drops into its
+--     @_ -> return ()@ arm (:172) and republishes (:174); the application
+--     forwards them here with 'verifyBlock' / 'verifyTx'.
+--
+-- Assumed dependency names (not checkable here): haskoin-core
+-- 'exportCompactSig' / 'exportPubKey' / 'txHash' / 'runPutS . serialize',
+-- secp256k1-haskell's 'CompactSig' bytes via 'getCompactSig'.
+module Haskoin.Node.Verify
+  ( VerifierConfig (..),
+    Verifier,
+    VerifierException (..),
+    withVerifier,
+    verifyRawBatch,
+    verifyHashSigBatch,
+    verifyStdInputBatch,
+    VerifyConfig (..),
+    VerifyEvent (..),
+    VerifyActor,
+    withVerifyActor,
+    verifyBlock,
+    verifyTx,
+  )
+where
+
+import Control.Monad (forM_, forever, when)
+import Control.Monad.Logger (MonadLoggerIO, logDebugS, logWarnS)
+import Crypto.Secp256k1 (getCompactSig)
+import Data.Bits (shiftR, testBit, (.&.))
+import Data.ByteString (ByteString)
+import qualified Data.ByteString as B
+import qualified Data.ByteString.Unsafe as BU
+import Data.Word (Word32, Word64, Word8)
+import Foreign.C.String (peekCString)
+import Foreign.Marshal.Alloc (alloca)
+import Foreign.Marshal.Array (allocaArray, peekArray, withArray)
+import Foreign.Marshal.Utils (copyBytes, fillBytes, with)
+import Foreign.Ptr (Ptr, castPtr, plusPtr)
+import Foreign.Storable (peek, pokeByteOff)
+import Haskoin
+  ( Block (..),
+    BlockHash,
+    Ctx,
+    Hash256,
+    Network,
+    PubKey,
+    ScriptOutput,
+    Sig,
+    Tx (..),
+    TxHash,
+    encodeOutputBS,
+    exportCompactSig,
+    exportPubKey,
+    getSigHashForkId,
+    headerHash,
+    runPutS,
+    serialize,
+    txHash,
+  )
+import Haskoin.Node.Verify.FFI
+import NQE (Mailbox, Publisher, newMailbox, publish, receive, send)
+import UnliftIO
+  ( Exception,
+    MVar,
+    MonadIO,
+    MonadUnliftIO,
+    bracket,
+    link,
+    liftIO,
+    newMVar,
+    throwIO,
+    withAsync,
+    withMVar,
+  )
+
+-- | Configuration, in the style of NodeConfig (Node.hs:74-96).
+data VerifierConfig = VerifierConfig
+  { -- | GPUs to shard every batch over (0: all visible)
+    gpus :: !Int,
+    -- | records per GPU call (the pinned host buffer's capacity)
+    maxBatch :: !Int
+  }
+
+data Verifier = Verifier
+  { ctx :: !(Ptr HkvCtx),
+    batch :: !(Ptr HkvBatch),
+    capacity :: !Int,
+    -- | one call at a time uses the pinned buffer
+    lock :: !(MVar ())
+  }
+
+-- | A device or argument error (a verdict is never an error).
+data VerifierException = VerifierException !String !Int
+  deriving (Show)
+
+instance Exception VerifierException
+
+check :: String -> Int -> IO ()
+check what rc = when (rc /= 0) $ do
+  msg <- peekCString =<< c_hkv_strerror (fromIntegral rc)
+  throwIO (VerifierException (what <> ": " <> msg) rc)
+
+-- | Open the GPUs, build the fixed-base tables, run the self-check; close on
+-- exit (secp256k1-haskell's createContext / withContext, batch-sized).
+withVerifier :: (MonadUnliftIO m) => VerifierConfig -> (Verifier -> m a) -> m a
+withVerifier cfg = bracket open close
+  where
+    open = liftIO $ do
+      c <- alloca $ \pc -> do
+        c_hkv_open (fromIntegral cfg.gpus) 0 pc >>= check "hkv_open" . fromIntegral
+        peek pc
+      b <- alloca $ \pb -> do
+        c_hkv_batch_alloc c (fromIntegral cfg.maxBatch) pb >>= check "hkv_batch_alloc" . fromIntegral
+        peek pb
+      l <- newMVar ()
+      return Verifier {ctx = c, batch = b, capacity = cfg.maxBatch, lock = l}
+    close v = liftIO $ do
+      c_hkv_batch_free v.batch
+      c_hkv_close v.ctx
+
+-- | Write one 168-byte record at @p@ (include/hkv.h):
+--   [0,32) msg32 | [32,64) r | [64,96) s | [96] pubkey length |
+--   [97,162) pubkey, zero padded | [162,168) zero.
+-- Malformed tuples are written as they are: the GPU rejects them exactly
+-- as secp256k1_ec_pubkey_parse / parse_compact would (a verdict, not an error).
+pokeRecord :: Ptr Word8 -> (ByteString, ByteString, ByteString) -> IO ()
+pokeRecord p (msg, sig, pub) = do
+  fillBytes p 0 hkvRecordSize
+  copyPrefix p 0 32 msg
+  copyPrefix p 32 64 sig
+  let pl = min 255 (B.length pub)
+  pokeByteOff p 96 (fromIntegral pl :: Word8)
+  copyPrefix p 97 65 pub
+  where
+    copyPrefix dst off n bs =
+      BU.unsafeUseAsCStringLen bs $ \(src, len) ->
+        copyBytes (dst `plusPtr` off) (castPtr src) (min n len)
+
+-- | Bit i of word i/32 is verdict i.
+readBits :: Int -> [Word32] -> [Bool]
+readBits n ws = [testBit (ws !! (i `shiftR` 5)) (i .&. 31) | i <- [0 .. n - 1]]
+
+-- | Raw (msg32, compact r||s, SEC1 pubkey bytes) tuples; mode 'hkvLibsecp'
+-- is secp256k1_ecdsa_verify, 'hkvHaskoin' is verifyHashSig. Batches larger
+-- than the buffer are split; each chunk is one blocking GPU call.
+verifyRawBatch :: Verifier -> Word32 -> [(ByteString, ByteString, ByteString)] -> IO [Bool]
+verifyRawBatch v mode = fmap concat . mapM one . chunks v.capacity
+  where
+    one xs = withMVar v.lock $ \_ -> do
+      let n = length xs
+          nw = (n + 31) `div` 32
+      recs <- c_hkv_batch_records v.batch
+      forM_ (zip [0 ..] xs) $ \(i, t) -> pokeRecord (recs `plusPtr` (i * hkvRecordSize)) t
+      allocaArray nw $ \bits -> do
+        c_hkv_verify v.ctx v.batch (fromIntegral n) mode bits >>= check "hkv_verify" . fromIntegral
+        readBits n <$> peekArray nw bits
+
+chunks :: Int -> [a] -> [[a]]
+chunks _ [] = []
+chunks k xs = let (a, b) = splitAt k xs in a : chunks k b
+
+-- | Element i equals @verifyHashSig ctx h_i s_i p_i@ (haskoin-core).
+verifyHashSigBatch :: Ctx -> Verifier -> [(Hash256, Sig, PubKey)] -> IO [Bool]
+verifyHashSigBatch c v xs =
+  verifyRawBatch v hkvHaskoin
+    [(runPutS (serialize h), getCompactSig (exportCompactSig c s), exportPubKey c True p) | (h, s, p) <- xs]
+
+-- | Element i equals @verifyStdInput net ctx tx_i input_i so_i value_i@ for
+-- P2PK / P2PKH / P2WPKH / P2SH-P2WPKH prevouts: template match, strict DER +
+-- low S (decodeTxSig), HASH160, txSigHash / txSigHashForkId and
+-- verifyHashSig all run on the GPU from the serialised txs.
+verifyStdInputBatch :: Verifier -> Network -> [Tx] -> [(Int, Int, ScriptOutput, Word64)] -> IO [Bool]
+verifyStdInputBatch v net txs ins = withMVar v.lock $ \_ -> do
+  let raws = map (runPutS . serialize) txs
+      offs = scanl (+) 0 (map (fromIntegral . B.length) raws) :: [Word32]
+      scripts = map (\(_, _, so, _) -> encodeOutputBS so) ins
+      soffs = scanl (+) 0 (map (fromIntegral . B.length) scripts) :: [Word32]
+      jobs =
+        [ InputJob (fromIntegral t) (fromIntegral i) so (fromIntegral (B.length s)) val
+          | ((t, i, _, val), s, so) <- zip3 ins scripts soffs
+        ]
+      forkid = maybe hkvNoForkId fromIntegral (getSigHashForkId net)
+      n = length ins
+      nw = (n + 31) `div` 32
+  BU.unsafeUseAsCString (B.concat raws) $ \pbytes ->
+    BU.unsafeUseAsCString (B.concat scripts) $ \pscripts ->
+      withArray offs $ \poffs ->
+        withArray jobs $ \pjobs ->
+          with (HkvTxs (castPtr pbytes) poffs (fromIntegral (length txs)) (castPtr pscripts) (last soffs)) $ \ptxs ->
+            allocaArray nw $ \bits -> do
+              c_hkv_verify_std_inputs v.ctx ptxs pjobs (fromIntegral n) forkid bits
+                >>= check "hkv_verify_std_inputs" . fromIntegral
+              readBits n <$> peekArray nw bits
+
+-- ---------------------------------------------------------------------------
+-- The Verify actor (withChain idiom, Chain.hs:277-307)
+
+-- | Where the prevouts come from: the node keeps no UTXO set (headers only,
+-- Chain.hs:209-231), so the application supplies (tx index, input index,
+-- prevout script, amount) for every input it wants checked.
+data VerifyConfig = VerifyConfig
+  { net :: !Network,
+    verifier :: !Verifier,
+    prevouts :: !(Block -> IO [(Int, Int, ScriptOutput, Word64)]),
+    txPrevouts :: !(Tx -> IO [(Int, ScriptOutput, Word64)]),
+    -- | verdicts are published here
+    pub :: !(Publisher VerifyEvent)
+  }
+
+data VerifyEvent
+  = BlockVerified !BlockHash
+  | BlockRejected !BlockHash ![(Int, Int)]
+  | TxVerified !TxHash
+  | TxRejected !TxHash ![Int]
+
+data VerifyMessage
+  = VerifyBlock !Block
+  | VerifyTx !Tx
+
+newtype VerifyActor = VerifyActor (Mailbox VerifyMessage)
+
+-- | Start the actor; it lives as long as the continuation.
+withVerifyActor :: (MonadUnliftIO m, MonadLoggerIO m) => VerifyConfig -> (VerifyActor -> m a) -> m a
+withVerifyActor cfg action = do
+  (inbox, mailbox) <- newMailbox
+  $(logDebugS) "Verify" "Starting verify actor"
+  withAsync (run inbox) $ \a -> link a >> action (VerifyActor mailbox)
+  where
+    run inbox = forever $ receive inbox >>= handle
+    handle (VerifyBlock b) = do
+      ins <- liftIO (cfg.prevouts b)
+      ok <- liftIO (verifyStdInputBatch cfg.verifier cfg.net b.txs ins)
+      let bad = [(t, i) | ((t, i, _, _), False) <- zip ins ok]
+          h = headerHash b.header
+      if null bad
+        then publish (BlockVerified h) cfg.pub
+        else do
+          $(logWarnS) "Verify" "Block has inputs that fail verifyStdInput"
+          publish (BlockRejected h bad) cfg.pub
+    handle (VerifyTx t) = do
+      ins <- liftIO (cfg.txPrevouts t)
+      ok <- liftIO (verifyStdInputBatch cfg.verifier cfg.net [t] [(0, i, so, val) | (i, so, val) <- ins])
+      let bad = [i | ((i, _, _), False) <- zip ins ok]
+      publish (if null bad then TxVerified (txHash t) else TxRejected (txHash t) bad) cfg.pub
+
+-- | Forward a block from PeerEvent (PeerMessage _ (MBlock b)) (Node.hs:172).
+verifyBlock :: (MonadIO m) => Block -> VerifyActor -> m ()
+verifyBlock b (VerifyActor mb) = VerifyBlock b `send` mb
+
+-- | Forward a transaction from PeerEvent (PeerMessage _ (MTx t)).
+verifyTx :: (MonadIO m) => Tx -> VerifyActor -> m ()
+verifyTx t (VerifyActor mb) = VerifyTx t `send` mb

@@ -44,3 +44,36 @@ def test_shard_bounds_partition(n, world):
         assert b[r][1] == b[r + 1][0]
         assert b[r][0] % 64 == 0 or b[r][0] == b[r][1]  # 64-aligned non-empty starts
     assert all(lo <= hi for lo, hi in b)
+
+
+def test_haskell_binding_layout_matches_ctypes_mirror():
+    """haskell/Haskoin/Node/Verify{,/FFI}.hs (uncompiled here: no GHC) and the
+    ctypes mirror (hkv/lib.py, hkv/records.py) describe the same bytes: the
+    Storable offsets of HkvTxs / InputJob equal the ctypes field offsets, and
+    pokeRecord's record offsets equal make_record's layout."""
+    import ctypes
+    import os
+    import re
+    from hkv.lib import HKV_RECORD_SIZE, HkvInputJob, HkvTxs
+    from hkv.records import make_record
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ffi = open(os.path.join(root, "haskell", "Haskoin", "Node", "Verify", "FFI.hs")).read()
+    ver = open(os.path.join(root, "haskell", "Haskoin", "Node", "Verify.hs")).read()
+
+    def poke_offsets(instance):
+        body = ffi[ffi.index(f"instance Storable {instance}"):]
+        body = body[:body.index("\n\n")]
+        size = int(re.search(r"sizeOf _ = (\d+)", body).group(1))
+        return size, [int(x) for x in re.findall(r"pokeByteOff p (\d+)", body)]
+
+    for inst, cstruct in (("HkvTxs", HkvTxs), ("InputJob", HkvInputJob)):
+        size, offs = poke_offsets(inst)
+        assert size == ctypes.sizeof(cstruct), inst
+        assert offs == [getattr(cstruct, f[0]).offset for f in cstruct._fields_], inst
+    assert f"hkvRecordSize = {HKV_RECORD_SIZE}" in ffi
+    # pokeRecord: msg32 at 0, r||s at 32, pubkey length byte at 96, key at 97 (<= 65 bytes)
+    assert "copyPrefix p 0 32 msg" in ver and "copyPrefix p 32 64 sig" in ver
+    assert "pokeByteOff p 96" in ver and "copyPrefix p 97 65 pub" in ver
+    rec = make_record(bytes(range(32)), bytes(range(32, 96)), b"\x02" + bytes(32))
+    assert rec[:32] == bytes(range(32)) and rec[32:96] == bytes(range(32, 96))
+    assert rec[96] == 33 and rec[97] == 2 and rec[130:] == bytes(HKV_RECORD_SIZE - 130)
