@@ -45,9 +45,16 @@ struct DevCtx {
   // tx index rows (hkv_sighash.hip) and host-API staging buffers
   uint32_t* txt = nullptr;
   size_t txt_cap = 0;  // bytes
-  // [0..3] tx batch, [4] sighash out, [5] header batch
+  // [0..3] tx batch, [4] sighash out, [5] header batch, [6] spare
   void* stage[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t stage_cap[7] = {0, 0, 0, 0, 0, 0, 0};
+  // multisig inputs (hkv_sighash.hip section 4): [0] desc words, [1] record
+  // totals (device), [2] offsets, [4] candidate + key records, [5] key bits,
+  // [6] host-form verdict words
+  void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t* ms_total = nullptr;  // pinned: off[n] (candidates | keys << 32)
+  hipEvent_t ms_ev = nullptr;
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -163,6 +170,8 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
   HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
   HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
+  HKV_TRY(hipEventCreateWithFlags(&d.ms_ev, hipEventDisableTiming), "hipEventCreate(multisig)");
+  HKV_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.ms_total), sizeof(uint64_t)), "hipHostMalloc(multisig)");
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
   HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
   HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 64 MiB at radix 2^20
@@ -197,6 +206,10 @@ void free_device(DevCtx& d) {
   if (d.txt) (void)hipFree(d.txt);
   for (auto p : d.stage)
     if (p) (void)hipFree(p);
+  for (auto p : d.ms)
+    if (p) (void)hipFree(p);
+  if (d.ms_total) (void)hipHostFree(d.ms_total);
+  if (d.ms_ev) (void)hipEventDestroy(d.ms_ev);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.clk) (void)hipFree(d.clk);
   if (d.last_use) (void)hipEventDestroy(d.last_use);
@@ -276,6 +289,53 @@ int enqueue_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, 
   HKV_TRY(hkv::launch_std_inputs(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
                                  static_cast<uint8_t*>(recs), st),
           "std input launch");
+  return HKV_OK;
+}
+
+// Full verifyStdInput over a job batch, verdict bit i -> out_bits (device).
+// Single-signature templates: one record per input (recs) through the verify
+// kernels. Multisig (bare / P2SH): the scan kernel's candidate counts are
+// summed on device and read back (the call waits for that 8-byte copy, which
+// runs ahead of the main verify); when there are any, their candidate and
+// key-check records are verified and hkv_ms_resolve_kernel ORs the verdicts
+// of the multisig inputs into out_bits.
+int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                              void* recs, uint32_t* out_bits, hipStream_t st) {
+  int rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  if (rc) return rc;
+  rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
+  if (!rc) rc = grow(&d.ms[1], &d.ms_cap[1], 8, "hipMalloc(multisig total)");
+  if (!rc) rc = grow(&d.ms[2], &d.ms_cap[2], n * 8, "hipMalloc(multisig offsets)");
+  if (rc) return rc;
+  uint32_t* desc = static_cast<uint32_t*>(d.ms[0]);
+  uint64_t* off = static_cast<uint64_t*>(d.ms[2]);
+  HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
+                              desc, off, static_cast<uint64_t*>(d.ms[1]), st),
+          "multisig scan launch");
+  HKV_TRY(hipMemcpyAsync(d.ms_total, d.ms[1], sizeof(uint64_t), hipMemcpyDeviceToHost, st), "D2H multisig total");
+  HKV_TRY(hipEventRecord(d.ms_ev, st), "hipEventRecord(multisig)");
+  rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st);
+  if (rc) return rc;
+  HKV_TRY(hipMemcpyAsync(out_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
+  HKV_TRY(hipEventSynchronize(d.ms_ev), "multisig total sync");
+  const uint64_t total = *d.ms_total;
+  const size_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
+  if (n_keys == 0) return HKV_OK;  // no multisig input
+  rc = grow(&d.ms[4], &d.ms_cap[4], (n_cand + n_keys) * hkv::REC_SIZE, "hipMalloc(multisig records)");
+  if (!rc) rc = grow(&d.ms[5], &d.ms_cap[5], round_up(n_keys, hkv::WG) / 8, "hipMalloc(multisig key bits)");
+  if (rc) return rc;
+  uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
+  uint8_t* keyrec = cand + n_cand * hkv::REC_SIZE;
+  uint32_t* kbits = static_cast<uint32_t*>(d.ms[5]);
+  HKV_TRY(hkv::launch_ms_emit(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
+                              desc, off, cand, keyrec, st),
+          "multisig emit launch");
+  HKV_TRY(hkv::launch_pubkey_check(keyrec, (uint32_t)n_keys, kbits, st), "pubkey check launch");
+  if (n_cand) {
+    rc = enqueue_verify(d, cand, n_cand, HKV_MODE_HASKOIN, st);
+    if (rc) return rc;
+  }
+  HKV_TRY(hkv::launch_ms_resolve(desc, off, (uint32_t)n, d.bits, kbits, out_bits, st), "multisig resolve launch");
   return HKV_OK;
 }
 
@@ -672,10 +732,8 @@ int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, co
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = scratch_acquire(d, st);
-  if (!rc) rc = enqueue_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, st);
-  if (!rc) rc = enqueue_verify(d, d_records, n, HKV_MODE_HASKOIN, st);
+  if (!rc) rc = enqueue_verify_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, d_bits, st);
   if (rc) return rc;
-  HKV_TRY(hipMemcpyAsync(d_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
   return scratch_release(d, st);
 }
 
@@ -698,10 +756,12 @@ int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job*
     HKV_TRY(hipMalloc(&d.recs, n * hkv::REC_SIZE), "hipMalloc(records)");
     d.recs_cap = n;
   }
-  if (!rc) rc = enqueue_std_inputs(d, &dt, static_cast<const hkv_input_job*>(djobs), n, forkid, d.recs, d.stream);
-  if (!rc) rc = enqueue_verify(d, d.recs, n, HKV_MODE_HASKOIN, d.stream);
+  if (!rc) rc = grow(&d.ms[6], &d.ms_cap[6], (n + 31) / 32 * 4, "hipMalloc(verdict words)");
+  if (!rc)
+    rc = enqueue_verify_std_inputs(d, &dt, static_cast<const hkv_input_job*>(djobs), n, forkid, d.recs,
+                                   static_cast<uint32_t*>(d.ms[6]), d.stream);
   if (rc) return rc;
-  HKV_TRY(hipMemcpyAsync(verdict_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
+  HKV_TRY(hipMemcpyAsync(verdict_bits, d.ms[6], (n + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
   HKV_TRY(hipStreamSynchronize(d.stream), "std inputs sync");
   return scratch_release(d, d.stream);
 }

@@ -48,6 +48,16 @@ hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt
 hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                              uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                              uint8_t* recs, hipStream_t st);
+// multisig inputs (hkv_sighash.hip section 4; pubkey check in hkv_kernels.hip)
+hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                          uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
+                          uint32_t* desc, uint64_t* off, uint64_t* total, hipStream_t st);
+hipError_t launch_ms_emit(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                          uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
+                          const uint32_t* desc, const uint64_t* off, uint8_t* cand, uint8_t* keyrec, hipStream_t st);
+hipError_t launch_ms_resolve(const uint32_t* desc, const uint64_t* off, uint32_t n, const uint32_t* cbits,
+                             const uint32_t* kbits, uint32_t* out_bits, hipStream_t st);
+hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st);
 // hkv_headers.hip
 hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
                           uint8_t* hashes, uint8_t* status, hipStream_t st);

@@ -50,6 +50,50 @@ __constant__ static const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC
 #ifndef HKV_PROLOGUE_WAVES
 #define HKV_PROLOGUE_WAVES 4  // min waves per SIMD the prologue's register allocation targets
 #endif
+
+// secp256k1_ec_pubkey_parse of the record's key (words 24..40: pklen,
+// SEC1 bytes): 02/03 + x (x < p, x^3 + 7 a square, y of the prefix's
+// parity), 04/06/07 + x, y (x, y < p, on the curve, 06/07 parity). Returns
+// the affine point in x, y (normalised). Call from wave-uniform control flow
+// (the sqrt is a wave-uniform branch).
+HKV_DEV bool pubkey_parse_rec(const uint32_t* w, fe& x, fe& y) {
+  const uint32_t pklen = w[24] & 0xFFu;
+  const uint32_t prefix = (w[24] >> 8) & 0xFFu;
+  const bool comp = (pklen == 33u) && (prefix == 2u || prefix == 3u);
+  const bool unc = (pklen == 65u) && (prefix == 4u || prefix == 6u || prefix == 7u);
+  fe rhs, t;
+  rec_be256(x.v, w, 98);
+  rec_be256(y.v, w, 130);
+  bool pk_ok = (comp || unc) && u256_lt_p(x.v);
+  if (unc) pk_ok = pk_ok && u256_lt_p(y.v);
+  fe_sqr(t, x);
+  fe_mul(t, t, x);
+  fe seven;
+  fe_set_u32(seven, 7);
+  fe_add(rhs, t, seven);
+  if (__any(comp)) {
+    fe yc, y2;
+    fe_sqrt_cand(yc, rhs);
+    fe_sqr(y2, yc);
+    const bool is_sq = fe_equal(y2, rhs);
+    fe_normalize(yc);
+    fe ny;
+    fe_neg(ny, yc);
+    fe_normalize(ny);
+    const bool flip = (yc.v[0] & 1u) != (prefix & 1u);
+    if (comp) {
+      pk_ok = pk_ok && is_sq;
+      y = flip ? ny : yc;
+    }
+  }
+  if (unc) {
+    fe y2;
+    fe_sqr(y2, y);
+    pk_ok = pk_ok && fe_equal(y2, rhs);
+    if (prefix != 4u) pk_ok = pk_ok && ((y.v[0] & 1u) == (prefix & 1u));  // hybrid parity
+  }
+  return pk_ok;
+}
 __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
                                                           uint32_t n_pad, uint32_t mode,
                                                           uint32_t* __restrict__ im) {
@@ -87,42 +131,8 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(co
   sc_cond_sub_n(m.v);  // m = msg32 mod n (msg32 < 2^256 < 2n)
 
   // --- pubkey: secp256k1_ec_pubkey_parse
-  const uint32_t pklen = w[24] & 0xFFu;
-  const uint32_t prefix = (w[24] >> 8) & 0xFFu;
-  const bool comp = (pklen == 33u) && (prefix == 2u || prefix == 3u);
-  const bool unc = (pklen == 65u) && (prefix == 4u || prefix == 6u || prefix == 7u);
-  fe x, y, rhs, t;
-  rec_be256(x.v, w, 98);
-  rec_be256(y.v, w, 130);
-  bool pk_ok = (comp || unc) && u256_lt_p(x.v);
-  if (unc) pk_ok = pk_ok && u256_lt_p(y.v);
-  fe_sqr(t, x);
-  fe_mul(t, t, x);
-  fe seven;
-  fe_set_u32(seven, 7);
-  fe_add(rhs, t, seven);
-  if (__any(comp)) {
-    fe yc, y2;
-    fe_sqrt_cand(yc, rhs);
-    fe_sqr(y2, yc);
-    const bool is_sq = fe_equal(y2, rhs);
-    fe_normalize(yc);
-    fe ny;
-    fe_neg(ny, yc);
-    fe_normalize(ny);
-    const bool flip = (yc.v[0] & 1u) != (prefix & 1u);
-    if (comp) {
-      pk_ok = pk_ok && is_sq;
-      y = flip ? ny : yc;
-    }
-  }
-  if (unc) {
-    fe y2;
-    fe_sqr(y2, y);
-    pk_ok = pk_ok && fe_equal(y2, rhs);
-    if (prefix != 4u) pk_ok = pk_ok && ((y.v[0] & 1u) == (prefix & 1u));  // hybrid parity
-  }
-  ok = ok && pk_ok;
+  fe x, y;
+  ok = pubkey_parse_rec(w, x, y) && ok;
 
   const uint32_t flags = ok ? FLAG_VALID : 0u;
   im[(size_t)IM_FLAGS * n_pad + i] = flags;
@@ -133,6 +143,30 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(co
     im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
     im[(size_t)(IM_S + k) * n_pad + i] = s.v[k];
     im[(size_t)(IM_M + k) * n_pad + i] = m.v[k];
+  }
+}
+
+// Key-only check (the keys of a CHECKMULTISIG script: haskoin-core decodes
+// every key with importPubKey, so one key off the curve fails the input
+// whatever its signatures do): bit i = record i's key parses. Bits leave as
+// one 64-bit ballot word per wave, like the verify kernel's.
+__global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_pubkey_check_kernel(const uint32_t* __restrict__ recs,
+                                                                                uint32_t n, uint32_t* __restrict__ bits) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  uint32_t w[REC_WORDS];
+#pragma unroll
+  for (int k = 0; k < REC_WORDS; ++k) w[k] = 0;
+  if (i < n) {
+#pragma unroll
+    for (int k = 24; k < 42; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
+  }
+  fe x, y;
+  const bool ok = pubkey_parse_rec(w, x, y) && i < n;
+  const uint64_t ball = __ballot(ok);
+  if ((threadIdx.x & 63) == 0) {
+    const uint32_t wbase = i & ~63u;
+    bits[wbase / 32] = (uint32_t)ball;
+    bits[wbase / 32 + 1] = (uint32_t)(ball >> 32);
   }
 }
 
@@ -875,6 +909,11 @@ hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const u
     hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, clk);
   else
     hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, clk);
+  return hipGetLastError();
+}
+hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(hkv_pubkey_check_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, (const uint32_t*)recs, n, bits);
   return hipGetLastError();
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {

@@ -753,6 +753,18 @@ HKV_DEV bool der_parse_sig(const uint8_t* p, uint32_t off, uint32_t end, uint32_
   if (!der_parse_int(p, off, end, s)) return false;
   return off == end;
 }
+// haskoin-core decodeTxSig: hashtype byte (known base type; FORKID only on a
+// fork-id network), then decodeStrictSig = DER parse + r, s != 0 + low S.
+HKV_DEV bool decode_tx_sig(const uint8_t* p, uint32_t off, uint32_t len, int32_t forkid, uint32_t r[8], uint32_t s[8],
+                           uint32_t& sh) {
+  if (len < 1) return false;
+  sh = p[off + len - 1];
+  const uint32_t base = sh & 0x1Fu;
+  if (!(base >= 1u && base <= 3u && !(forkid < 0 && (sh & 0x40u)))) return false;
+  if (!der_parse_sig(p, off, off + len - 1, r, s)) return false;
+  return !u256_is_zero(r) && !u256_is_zero(s) && !u256_lt(SC_HALF_N, s);
+}
+
 // one data push (opcodes 1..78) at off within [off, end): data range
 HKV_DEV bool read_push(const uint8_t* p, uint32_t& off, uint32_t end, uint32_t& d_off, uint32_t& d_len) {
   if (off >= end) return false;
@@ -864,19 +876,7 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
         }
       }
     }
-    // decodeTxSig: strict DER + r, s != 0 + low S, then the hashtype byte
-    if (ok) {
-      ok = sig_len >= 1;
-      if (ok) {
-        sh = txs[sig_off + sig_len - 1];
-        const uint32_t base = sh & 0x1Fu;
-        ok = base >= 1u && base <= 3u && !(forkid < 0 && (sh & 0x40u));
-      }
-      if (ok) {
-        ok = der_parse_sig(txs, sig_off, sig_off + sig_len - 1, r, s);
-        ok = ok && !u256_is_zero(r) && !u256_is_zero(s) && !u256_lt(SC_HALF_N, s);
-      }
-    }
+    if (ok) ok = decode_tx_sig(txs, sig_off, sig_len, forkid, r, s, sh);
     // haskoin PubKeyI encoding
     if (ok) ok = (pub_len == 33 && (pub[0] == 2u || pub[0] == 3u)) || (pub_len == 65 && pub[0] == 4u);
   }
@@ -965,6 +965,336 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// 4. multisig inputs (bare and P2SH): candidate (signature, key) records
+// ---------------------------------------------------------------------------
+// haskoin-core verifyStdInput's PayMulSig branch [dep; oracle/sighash_oracle.py
+// std_multisig]: countMulSig walks the keys in order against the current
+// signature; a match consumes both, a miss only the key, an empty signature
+// (OP_0) one of each; the input verifies iff the count equals m and every
+// key of the script is a point (importPubKey). Which comparisons the walk
+// makes depends on earlier verdicts, so the batch checks every pair it could
+// make (signature j < min(#sigs, n) against keys j..n-1) and
+// hkv_ms_resolve_kernel replays the walk over the verdict bits.
+//   hkv_ms_scan_kernel    per input: template + scriptSig decode (+ the P2SH
+//                         redeem HASH160), desc words and candidate counts
+//   (exclusive scan of the counts -> record offsets)
+//   hkv_ms_emit_kernel    per input: sighash of each signature, candidate and
+//                         key-check records
+//   hkv_ms_resolve_kernel per input: the countMulSig walk -> verdict bit
+// Keys must be direct pushes (21 / 41) with PubKeyI prefixes, the limit the
+// P2PK template shares, so haskoin's canonical re-encoding (encodeOutput) of
+// the script equals its bytes.
+constexpr uint32_t MS_OK = 1u << 31, MS_P2SH = 1u << 30;
+
+// OP_m <keys> OP_n OP_CHECKMULTISIG, 1 <= m <= n <= 16
+HKV_DEV bool ms_template(const uint8_t* sc, uint32_t L, uint32_t& m, uint32_t& n) {
+  if (L < 3 || sc[L - 1] != 0xAEu) return false;
+  m = (uint32_t)sc[0] - 0x50u;
+  n = (uint32_t)sc[L - 2] - 0x50u;
+  if (m < 1u || m > 16u || n < 1u || n > 16u || m > n) return false;
+  uint32_t off = 1, k = 0;
+  while (off < L - 2 && k < 17u) {
+    const uint32_t op = sc[off];
+    if (op != 0x21u && op != 0x41u) return false;
+    if (off + 1 + op > L - 2) return false;
+    const uint32_t pre = sc[off + 1];
+    if (op == 0x21u ? (pre != 2u && pre != 3u) : (pre != 4u)) return false;
+    off += 1 + op;
+    ++k;
+  }
+  return off == L - 2 && k == n;
+}
+// key k of a validated template
+HKV_DEV const uint8_t* ms_key(const uint8_t* sc, uint32_t k, uint32_t& len) {
+  uint32_t off = 1;
+  for (uint32_t q = 0; q < k; ++q) off += 1 + sc[off];
+  len = sc[off];
+  return sc + off + 1;
+}
+// skip one script op (haskoin's Script parse: a push must fit)
+HKV_DEV bool skip_op(const uint8_t* p, uint32_t& off, uint32_t end) {
+  const uint32_t op = p[off];
+  if (op == 0u || op > 0x4Eu) {
+    ++off;
+    return true;
+  }
+  uint32_t d_off, d_len;
+  return read_push(p, off, end, d_off, d_len);
+}
+
+struct MsIn {
+  const uint8_t* code;  // scriptCode: the prevout script (bare) or the redeem script (P2SH)
+  uint32_t code_len;
+  uint32_t it_off, it_end;  // the signature items (after the OP_0 dummy, before the redeem push)
+  uint32_t m, n, s_eff, mask, n_cand;
+  bool p2sh;
+};
+
+// decode a multisig input except the P2SH redeem HASH160 (needs SHA-256)
+HKV_DEV bool ms_parse(MsIn& r, const uint8_t* txs, const uint32_t* row, uint32_t input, const uint8_t* spk,
+                      uint32_t L, int32_t forkid) {
+  r.p2sh = L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u;
+  uint32_t in_off, ss_off, ss_len, seq_off;
+  walk_input(txs, row[TXT_INS], input, in_off, ss_off, ss_len, seq_off);
+  const uint32_t end = ss_off + ss_len;
+  if (ss_len == 0 || txs[ss_off] != 0u) return false;  // haskoin matchMulSig: OP_0 first
+  r.it_off = ss_off + 1;
+  if (r.p2sh) {
+    uint32_t off = ss_off + 1, last = 0, n_ops = 0;
+    while (off < end) {
+      last = off;
+      if (!skip_op(txs, off, end)) return false;
+      ++n_ops;
+    }
+    if (n_ops == 0) return false;
+    uint32_t c = last, d_off = 0, d_len = 0;
+    if (!read_push(txs, c, end, d_off, d_len)) return false;  // the redeem script: OP_PUSHDATA
+    r.code = txs + d_off;
+    r.code_len = d_len;
+    r.it_end = last;
+  } else {
+    r.code = spk;
+    r.code_len = L;
+    r.it_end = end;
+  }
+  if (!ms_template(r.code, r.code_len, r.m, r.n)) return false;
+  uint32_t j = 0, mask = 0, cand = 0, off = r.it_off;
+  while (off < r.it_end) {
+    if (txs[off] == 0u) {
+      ++off;  // OP_0: TxSignatureEmpty
+    } else {
+      uint32_t d_off = 0, d_len = 0;
+      if (!read_push(txs, off, r.it_end, d_off, d_len)) return false;  // any other op fails the decode
+      if (d_len) {
+        uint32_t rr[8], ss[8], sh;
+        if (!decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh)) return false;
+        if (j < r.n) {
+          mask |= 1u << j;
+          cand += r.n - j;
+        }
+      }
+    }
+    ++j;
+  }
+  r.s_eff = j < r.n ? j : r.n;
+  r.mask = mask;
+  r.n_cand = cand;
+  return true;
+}
+
+// job -> (row, prevout script); false for a bad reference / unparsed tx
+HKV_DEV bool ms_job(const hkv_input_job& jb, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                    uint32_t scripts_len, const uint32_t*& row, const uint8_t*& spk) {
+  if (!(jb.tx < n_tx && jb.script_off <= scripts_len && scripts_len - jb.script_off >= jb.script_len)) return false;
+  row = txt + (size_t)jb.tx * TXT_WORDS;
+  if (!((row[TXT_FLAGS] & TXF_OK) && jb.input < row[TXT_NIN])) return false;
+  spk = scripts + jb.script_off;
+  return true;
+}
+
+__global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
+                                                         const uint32_t* __restrict__ txt,
+                                                         const uint8_t* __restrict__ scripts, uint32_t scripts_len,
+                                                         const hkv_input_job* __restrict__ jobs, uint32_t n,
+                                                         int32_t forkid, uint32_t* __restrict__ desc,
+                                                         uint64_t* __restrict__ off,
+                                                         unsigned long long* __restrict__ total) {
+  __shared__ uint32_t buf[16 * WG];
+  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
+  MsIn r;
+  r.p2sh = false;
+  r.code = scripts;
+  r.code_len = 0;
+  bool ok = false;
+  const uint8_t* spk = scripts;
+  if (jx < n) {
+    const hkv_input_job jb = jobs[jx];
+    const uint32_t* row = txt;
+    ok = ms_job(jb, n_tx, txt, scripts, scripts_len, row, spk);
+    if (ok) {
+      const uint32_t L = jb.script_len;
+      const bool p2sh = L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u;
+      const bool bare = L >= 3u && spk[L - 1] == 0xAEu;
+      ok = (p2sh || bare) && ms_parse(r, txs, row, jb.input, spk, L, forkid);
+    }
+  }
+  // P2SH: HASH160(redeem script) == the script hash
+  const bool need = ok && r.p2sh;
+  if (__any(need)) {
+    Gen g;
+    uint32_t h[8];
+    gen_clear(g);
+    g.code = r.code;
+    g.code_len = r.code_len;
+    g.phase = PH_RANGE;
+    sha256_stream(h, g, need, buf);
+    uint32_t rip[5];
+    ripemd160_of_digest(rip, h);
+    if (need) {
+      const uint8_t* hp20 = spk + 2;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t want = hp20[4 * k] | (hp20[4 * k + 1] << 8) | (hp20[4 * k + 2] << 16) |
+                              ((uint32_t)hp20[4 * k + 3] << 24);
+        ok = ok && want == rip[k];
+      }
+    }
+  }
+  if (jx < n) {
+    desc[2 * (size_t)jx] = ok ? (MS_OK | (r.p2sh ? MS_P2SH : 0u) | r.m | (r.n << 8) | (r.s_eff << 16)) : 0u;
+    desc[2 * (size_t)jx + 1] = ok ? r.mask : 0u;
+    // record ranges: candidates in the low 32 bits, key checks in the high 32
+    // (their sums stay below 2^32); placement order is irrelevant to verdicts
+    off[jx] = ok ? (uint64_t)atomicAdd(total, (unsigned long long)r.n_cand | ((unsigned long long)r.n << 32)) : 0ull;
+  }
+}
+
+// record: msg32 (digest byte order words) | r | s (limbs, written big-endian) |
+// pklen | pubkey | zero padding
+HKV_DEV void write_record(uint32_t* r32, const uint32_t msg[8], const uint32_t r[8], const uint32_t s[8],
+                          const uint8_t* pub, uint32_t pub_len) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r32[k] = msg[k];
+    r32[8 + k] = __builtin_bswap32(r[7 - k]);
+    r32[16 + k] = __builtin_bswap32(s[7 - k]);
+  }
+#pragma unroll
+  for (int w = 0; w < 18; ++w) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int q = 4 * w + b;  // byte 96 + q of the record
+      uint32_t byte = 0;
+      if (q == 0) byte = pub_len;
+      else if ((uint32_t)(q - 1) < pub_len && q - 1 < 65) byte = pub[q - 1];
+      v |= byte << (8 * b);
+    }
+    r32[24 + w] = v;
+  }
+}
+
+__global__ void __launch_bounds__(WG) hkv_ms_emit_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
+                                                         const uint32_t* __restrict__ txt,
+                                                         const uint8_t* __restrict__ scripts, uint32_t scripts_len,
+                                                         const hkv_input_job* __restrict__ jobs, uint32_t n,
+                                                         int32_t forkid, const uint32_t* __restrict__ desc,
+                                                         const uint64_t* __restrict__ off64,
+                                                         uint8_t* __restrict__ cand, uint8_t* __restrict__ keyrec) {
+  __shared__ uint32_t buf[16 * WG];
+  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
+  bool go = jx < n && (desc[2 * (size_t)jx] & MS_OK);
+  MsIn r;
+  r.code = scripts; r.code_len = 0; r.s_eff = 0; r.mask = 0; r.n = 0; r.it_off = r.it_end = 0;
+  const uint32_t* row = txt;
+  const uint8_t* spk = scripts;
+  uint32_t input = 0;
+  uint64_t value = 0;
+  uint32_t cbase = 0, kbase = 0;
+  if (go) {
+    const hkv_input_job jb = jobs[jx];
+    input = jb.input;
+    value = jb.value;
+    go = ms_job(jb, n_tx, txt, scripts, scripts_len, row, spk) &&
+         ms_parse(r, txs, row, jb.input, spk, jb.script_len, forkid);
+    const uint64_t o = off64[jx];
+    cbase = (uint32_t)o;
+    kbase = (uint32_t)(o >> 32);
+  }
+  // key-check records (msg, r, s zero): one per key of the script
+  if (go) {
+    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t k = 0; k < r.n; ++k) {
+      uint32_t kl;
+      const uint8_t* kp = ms_key(r.code, k, kl);
+      write_record(reinterpret_cast<uint32_t*>(keyrec + (size_t)(kbase + k) * REC_SIZE), z, z, z, kp, kl);
+    }
+  }
+  // per signature j < s_eff: its sighash, then records (msg_j, r_j, s_j, key_k), k = j..n-1
+  uint32_t off = r.it_off, idx = cbase;
+  Gen g;
+  uint32_t h[8], d[8];
+  for (uint32_t j = 0; __any(go && j < r.s_eff); ++j) {
+    const bool here = go && j < r.s_eff;
+    uint32_t d_off = 0, d_len = 0;
+    if (here) {
+      if (txs[off] == 0u) ++off;
+      else (void)read_push(txs, off, r.it_end, d_off, d_len);
+    }
+    const bool live = here && ((r.mask >> j) & 1u);
+    uint32_t rr[8], ss[8], sh = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rr[k] = ss[k] = 0;
+    if (live) (void)decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh);
+    JobCtx c;
+    c.forkid_form = false; c.one = false; c.single_hash = false;
+    if (live) job_setup(c, txs, row, input, sh, false, forkid);
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(cand + (size_t)idx * REC_SIZE);  // first record of sig j
+    const bool need_single = live && c.single_hash;
+    if (__any(need_single)) {
+      gen_clear(g);
+      g.T = txs; g.ooff = c.single_off; g.ocnt = 1; g.ret = PH_DONE; g.phase = PH_O_VAL;
+      sha256_stream(h, g, need_single, buf);
+      sha256d_finish(d, h);
+      if (need_single) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r32[k] = d[k];  // scratch: hashOutputs of output i
+      }
+    }
+    const bool hashed = live && !c.one;
+    if (hashed) gen_job(g, c, txs, row, r.code, r.code_len, false, value, r32);
+    else gen_clear(g);
+    sha256_stream(h, g, hashed, buf);
+    sha256d_finish(d, h);
+    if (live) {
+      uint32_t msg[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) msg[k] = hashed ? d[k] : (k == 0 ? 1u : 0u);
+      for (uint32_t k = j; k < r.n; ++k) {
+        uint32_t kl;
+        const uint8_t* kp = ms_key(r.code, k, kl);
+        write_record(reinterpret_cast<uint32_t*>(cand + (size_t)(idx++) * REC_SIZE), msg, rr, ss, kp, kl);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool bit_at(const uint32_t* b, uint32_t i) { return (b[i >> 5] >> (i & 31u)) & 1u; }
+
+__global__ void __launch_bounds__(WG) hkv_ms_resolve_kernel(const uint32_t* __restrict__ desc,
+                                                            const uint64_t* __restrict__ off64, uint32_t n,
+                                                            const uint32_t* __restrict__ cbits,
+                                                            const uint32_t* __restrict__ kbits,
+                                                            uint32_t* __restrict__ out_bits) {
+  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
+  if (jx >= n) return;
+  const uint32_t d0 = desc[2 * (size_t)jx];
+  if (!(d0 & MS_OK)) return;
+  const uint32_t mask = desc[2 * (size_t)jx + 1];
+  const uint32_t m = d0 & 0xFFu, nk = (d0 >> 8) & 0xFFu, s_eff = (d0 >> 16) & 0xFFu;
+  const uint64_t o = off64[jx];
+  uint32_t start = (uint32_t)o;
+  const uint32_t kbase = (uint32_t)(o >> 32);
+  bool keys_ok = true;
+  for (uint32_t k = 0; k < nk; ++k) keys_ok = keys_ok && bit_at(kbits, kbase + k);
+  // countMulSig': start = index of candidate (j, j)
+  uint32_t count = 0, j = 0;
+  for (uint32_t k = 0; k < nk; ++k) {
+    if (j >= s_eff) break;
+    if (!((mask >> j) & 1u)) {  // TxSignatureEmpty: consumes the key and the signature
+      ++j;
+      continue;
+    }
+    if (bit_at(cbits, start + (k - j))) {
+      ++count;
+      start += nk - j;
+      ++j;
+    }
+  }
+  if (keys_ok && count == m) atomicOr(&out_bits[jx >> 5], 1u << (jx & 31u));
+}
+
 }  // namespace hkv
 
 // ---------------------------------------------------------------------------
@@ -998,6 +1328,38 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(hkv_std_input_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts,
                      scripts_len, jobs, n, forkid, recs);
+  return hipGetLastError();
+}
+
+}  // namespace hkv
+
+// ---------------------------------------------------------------------------
+// multisig launch wrappers
+// ---------------------------------------------------------------------------
+namespace hkv {
+
+// per-input desc words and record offsets; *total (zeroed here) ends as the
+// number of candidate records | key-check records << 32
+hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                          uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
+                          uint32_t* desc, uint64_t* off, uint64_t* total, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hkv_ms_scan_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts, scripts_len,
+                     jobs, n, forkid, desc, off, reinterpret_cast<unsigned long long*>(total));
+  return hipGetLastError();
+}
+hipError_t launch_ms_emit(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                          uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
+                          const uint32_t* desc, const uint64_t* off, uint8_t* cand, uint8_t* keyrec, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_ms_emit_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts, scripts_len,
+                     jobs, n, forkid, desc, off, cand, keyrec);
+  return hipGetLastError();
+}
+hipError_t launch_ms_resolve(const uint32_t* desc, const uint64_t* off, uint32_t n, const uint32_t* cbits,
+                             const uint32_t* kbits, uint32_t* out_bits, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_ms_resolve_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, desc, off, n, cbits, kbits,
+                     out_bits);
   return hipGetLastError();
 }
 

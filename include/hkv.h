@@ -28,9 +28,10 @@
  *   hkv_verify_std_inputs / hkv_verify_std_inputs_device
  *       replaces N calls of haskoin-core
  *       `verifyStdInput :: Network -> Ctx -> Tx -> Int -> ScriptOutput -> Word64 -> Bool`
- *       (Haskoin.Transaction.Builder) for P2PK / P2PKH / P2WPKH prevouts:
- *       decodeTxSig (strict DER, low S, hashtype), HASH160 check, sighash and
- *       verifyHashSig, all on device.
+ *       (Haskoin.Transaction.Builder) for P2PK / P2PKH / P2WPKH /
+ *       P2SH-P2WPKH and bare / P2SH multisig prevouts: decodeTxSig (strict
+ *       DER, low S, hashtype), HASH160 check, sighash, verifyHashSig and the
+ *       countMulSig walk, all on device.
  *   hkv_check_headers / hkv_check_headers_device
  *       replaces the per-header part of haskoin-core `connectBlocks` reached
  *       from importHeaders (/root/reference/src/Haskoin/Node/Chain.hs:500-520):
@@ -167,8 +168,10 @@ typedef struct hkv_sighash_job {
 
 /* One standard input for verifyStdInput: input `input` of tx `tx` spends a
  * prevout with scriptPubKey = scripts[script_off, +script_len) and amount
- * `value`. Templates: P2PK (21 <33> ac / 41 <65> ac), P2PKH, P2WPKH; any other
- * prevout script verifies false. 24 bytes. */
+ * `value`. Templates: P2PK (21 <33> ac / 41 <65> ac), P2PKH, P2WPKH,
+ * P2SH-P2WPKH, bare multisig (OP_m <keys> OP_n OP_CHECKMULTISIG, keys as
+ * direct 21 / 41 pushes) and P2SH multisig (the same script as the redeem
+ * script); any other prevout script verifies false. 24 bytes. */
 typedef struct hkv_input_job {
   uint32_t tx;
   uint32_t input;
@@ -188,12 +191,19 @@ int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, s
 int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_sighash_job* d_jobs, size_t n,
                        int32_t forkid, uint8_t* d_out, size_t out_stride, uint8_t* d_status, void* hip_stream);
 /* The non-ECDSA half of verifyStdInput on device: one 168-byte verify record
- * per input (all-zero when the template / DER / HASH160 checks fail). */
+ * per single-signature input (all-zero when the template / DER / HASH160
+ * checks fail, and for multisig inputs, which only the verify entry points
+ * below resolve). */
 int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                           int32_t forkid, void* d_records, void* hip_stream);
 /* Full batch verifyStdInput: extraction + ECDSA (HKV_HASKOIN semantics).
  * d_records: scratch of n * 168 bytes; verdict bit i in d_bits
- * (>= ceil(n/64)*2 words). Enqueued on hip_stream, not synchronised. */
+ * (>= ceil(n/64)*2 words). Multisig inputs follow haskoin-core countMulSig:
+ * every (signature j, key k >= j) pair the walk could compare is verified as
+ * its own record, every key of the script is parse-checked, and a resolve
+ * kernel replays the walk (count == m and all keys valid). Enqueued on
+ * hip_stream; the call itself waits only for the 8-byte count of multisig
+ * records (read back ahead of the main verify), not for the verdicts. */
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                                  int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream);
 /* Host-memory form of the above; writes ceil(n/32) verdict words. Blocking. */

@@ -604,12 +604,178 @@ def std_input(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[i
     return StdInput(False)
 
 
+def _record(msg32: bytes, r: int, s: int, pub: bytes) -> bytes:
+    rec = msg32 + r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([len(pub)]) + pub.ljust(65, b"\x00")
+    return rec.ljust(168, b"\x00")
+
+
 def std_input_record(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[int] = None) -> bytes:
     """The 168-byte verify record the device extractor must produce (an
-    all-zero record when the template checks fail)."""
+    all-zero record when the template checks fail, and for multisig inputs,
+    which are resolved from candidate records instead: std_multisig)."""
     si = std_input(tx, i, prev_script, value, forkid)
     if not si.ok:
         return b"\x00" * 168
-    rec = si.msg32 + si.r.to_bytes(32, "big") + si.s.to_bytes(32, "big") + bytes([len(si.pubkey)]) \
-        + si.pubkey.ljust(65, b"\x00")
-    return rec.ljust(168, b"\x00")
+    return _record(si.msg32, si.r, si.s, si.pubkey)
+
+
+# --- multisig: bare and P2SH (haskoin-core verifyStdInput's PayMulSig branch) ----
+#
+# haskoin-core-1.1.0 [dep, stack.yaml:10] Haskoin.Transaction.Builder:
+#   verifyStdInput ... (PayMulSig pubs r) (SpendMulSig sigs) = countMulSig ... pubs sigs == r
+#   countMulSig' _ [] _ = 0
+#   countMulSig' _ _ [] = 0
+#   countMulSig' h (_ : pubs) (TxSignatureEmpty : sigs) = countMulSig' h pubs sigs
+#   countMulSig' h (PubKeyI pub _ : pubs) sigs@(TxSignature sig sh : sigs')
+#     | verifyHashSig (h sh) sig pub = 1 + countMulSig' h pubs sigs'
+#     | otherwise = countMulSig' h pubs sigs
+# with h sh = txSigHash net tx (encodeOutput so) value i sh. Decoding
+# (Haskoin.Script.Standard): the output must be OP_m <keys> OP_n
+# OP_CHECKMULTISIG, 1 <= m <= n <= 16, n keys that deserialise as PubKeyI
+# (02/03 + 32 bytes or 04 + 64 bytes AND a point on the curve, importPubKey);
+# the input must be OP_0 followed by items that are OP_0 / empty pushes
+# (TxSignatureEmpty) or decodeTxSig-valid signatures (any other item fails the
+# whole decode). P2SH: the scriptSig's last op is a push of the redeem script,
+# which must decode as the multisig output and whose HASH160 is the P2SH hash;
+# the scriptCode is then the redeem script. Parity with the reference stack is
+# unpinned by data (the reference fixtures hold no multisig); deliberate limit
+# shared with P2PK: keys must be direct pushes (21 / 41), so encodeOutput's
+# canonical re-encoding equals the script bytes.
+
+def multisig_template(script: bytes) -> Optional[Tuple[int, List[bytes]]]:
+    """(m, keys) of a canonical OP_m <k_1..k_n> OP_n OP_CHECKMULTISIG script."""
+    L = len(script)
+    if L < 3 or script[-1] != 0xAE:
+        return None
+    m, n = script[0] - 0x50, script[-2] - 0x50
+    if not (1 <= m <= 16 and 1 <= n <= 16 and m <= n):
+        return None
+    keys, off = [], 1
+    while off < L - 2:
+        op = script[off]
+        if op not in (0x21, 0x41) or off + 1 + op > L - 2:
+            return None
+        k = script[off + 1:off + 1 + op]
+        if not pubkey_bytes_ok(k):
+            return None
+        keys.append(k)
+        off += 1 + op
+    if off != L - 2 or len(keys) != n:
+        return None
+    return m, keys
+
+
+def _multisig_items(script: bytes, p2sh: bool) -> Optional[Tuple[List[Optional[bytes]], bytes]]:
+    """scriptSig -> (items, redeem): items are None for OP_0 / empty pushes;
+    the first op must be OP_0 (the CHECKMULTISIG dummy, haskoin matchMulSig)."""
+    ops = script_ops(script)
+    if ops is None or len(ops) < (2 if p2sh else 1) or script[ops[0][0]] != 0x00:
+        return None
+    redeem = b""
+    body = ops[1:]
+    if p2sh:
+        last = _push_items(script[ops[-1][0]:ops[-1][1]])
+        if last is None or len(last) != 1:
+            return None
+        redeem = last[0]
+        body = ops[1:-1]
+    items: List[Optional[bytes]] = []
+    for a, e in body:
+        if script[a] == 0x00:
+            items.append(None)
+            continue
+        d = _push_items(script[a:e])
+        if d is None:
+            return None
+        items.append(d[0] if d[0] else None)
+    return items, redeem
+
+
+@dataclass
+class MultiSig:
+    """A structurally valid multisig input: what the batch path verifies."""
+    m: int
+    keys: List[bytes]
+    sigs: List[Optional[Tuple[int, int, int]]]   # (r, s, sighash) or None (empty)
+    msgs: List[bytes]                             # sighash of sig j (j < min(#sigs, n)), ZERO32 if empty
+
+    def candidates(self) -> List[Tuple[int, int]]:
+        """(sig j, key k) pairs the CHECKMULTISIG walk can compare, in the
+        device's order: nonempty j < min(#sigs, n), then k = j .. n-1."""
+        n = len(self.keys)
+        return [(j, k) for j in range(min(len(self.sigs), n)) if self.sigs[j] is not None for k in range(j, n)]
+
+    def candidate_records(self) -> List[bytes]:
+        return [_record(self.msgs[j], self.sigs[j][0], self.sigs[j][1], self.keys[k]) for j, k in self.candidates()]
+
+    def key_records(self) -> List[bytes]:
+        return [_record(ZERO32, 0, 0, k) for k in self.keys]
+
+    def resolve(self, cand_ok: List[bool], keys_ok: List[bool]) -> bool:
+        """countMulSig' over the candidate verdicts; all keys must be points."""
+        if not all(keys_ok):
+            return False
+        idx = {c: v for c, v in zip(self.candidates(), cand_ok)}
+        count, j = 0, 0
+        for k in range(len(self.keys)):
+            if j >= len(self.sigs):
+                break
+            if self.sigs[j] is None:
+                j += 1
+                continue
+            if idx[(j, k)]:
+                count += 1
+                j += 1
+        return count == self.m
+
+
+def std_multisig(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[int] = None
+                 ) -> Optional[MultiSig]:
+    """Decode a bare or P2SH multisig input (None: not one, or it fails to
+    decode, i.e. verifyStdInput is False)."""
+    if i >= len(tx.inputs):
+        return None
+    p2sh = len(prev_script) == 23 and prev_script[:2] == b"\xa9\x14" and prev_script[22] == 0x87
+    if p2sh:
+        it = _multisig_items(tx.inputs[i].script, True)
+        if it is None:
+            return None
+        items, code = it
+        if hash160(code) != prev_script[2:22]:
+            return None
+    else:
+        code = prev_script
+        it = _multisig_items(tx.inputs[i].script, False)
+        if it is None:
+            return None
+        items = it[0]
+    tmpl = multisig_template(code)
+    if tmpl is None:
+        return None
+    m, keys = tmpl
+    sigs: List[Optional[Tuple[int, int, int]]] = []
+    for item in items:
+        if item is None:
+            sigs.append(None)
+            continue
+        ts = decode_tx_sig(item, forkid)
+        if ts is None:
+            return None
+        sigs.append(ts)
+    msgs = []
+    for j in range(min(len(sigs), len(keys))):
+        msgs.append(ZERO32 if sigs[j] is None else sighash_legacy(tx, code, value, i, sigs[j][2], forkid))
+    return MultiSig(m, keys, sigs, msgs)
+
+
+def verify_std_input(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[int], verify_records,
+                     key_ok) -> bool:
+    """Full verifyStdInput verdict. verify_records(list of records) -> list of
+    bools (HASKOIN-mode ECDSA, e.g. the C oracle); key_ok(pubkey bytes) ->
+    importPubKey succeeds."""
+    ms = std_multisig(tx, i, prev_script, value, forkid)
+    if ms is not None:
+        cands = ms.candidate_records()
+        return ms.resolve(list(verify_records(cands)) if cands else [], [key_ok(k) for k in ms.keys])
+    rec = std_input_record(tx, i, prev_script, value, forkid)
+    return bool(verify_records([rec])[0])

@@ -314,3 +314,87 @@ def test_p2pkh_block_config0(torch, ver, coracle, openssl):
         flips.append(2 * t + i)
     got = _block_vs_oracle(torch, ver, coracle, openssl, bad_txs, inputs)
     assert [k for k, v in enumerate(got) if not v] == flips
+
+
+# --- multisig (bare and P2SH) ---------------------------------------------------
+
+def _ms_oracle(coracle, txs, jobs, forkid):
+    from test_sighash_oracle import multisig_verdicts
+    return multisig_verdicts(coracle, [sh.tx_parse(t) for t in txs], jobs, forkid)
+
+
+def _device_verify_std(torch, ver, raw_txs, inputs, forkid):
+    """hkv_verify_std_inputs_device over HBM-resident txs / jobs."""
+    import hkv
+    from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
+    tb = TxBatch(raw_txs)
+    arr = np.zeros(len(inputs), dtype=INPUT_JOB_DTYPE)
+    for k, (t, i, spk, value) in enumerate(inputs):
+        off, ln = tb.script(spk)
+        arr[k] = (t, i, off, ln, value)
+    _, pool = tb.struct()
+    d_bytes, d_off, d_pool, d_jobs = upload(torch, tb.bytes), upload(torch, tb.offsets), upload(torch, pool), \
+        upload(torch, arr)
+    dt = hkv.HkvTxs(d_bytes.data_ptr(), d_off.data_ptr(), len(raw_txs), d_pool.data_ptr(), tb._len)
+    recs = torch.zeros(len(inputs) * 168, dtype=torch.uint8, device="cuda")
+    bits = torch.zeros(((len(inputs) + 63) // 64) * 2, dtype=torch.int32, device="cuda")
+    ver.verify_std_inputs_device(0, dt, d_jobs.data_ptr(), len(inputs), -1 if forkid is None else forkid,
+                                 recs.data_ptr(), bits.data_ptr())
+    torch.cuda.synchronize()
+    w = bits.cpu().numpy().view(np.uint32)
+    return [bool((w[k // 32] >> (k % 32)) & 1) for k in range(len(inputs))]
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_multisig_inputs_vs_oracle(torch, ver, coracle, forkid):
+    """Bare and P2SH m-of-n inputs (1-of-1 .. 15-of-15, 1-of-16; 22 valid and
+    adversarial variants, tests/txgen.py multisig_cases) shuffled into a
+    signed single-signature block: verdicts of the host and device entry
+    points equal the oracle's countMulSig walk over C-oracle candidate
+    verdicts, and the single-signature inputs are unaffected."""
+    import hkv
+    rng = random.Random(177 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(24)]
+    mtxs, mjobs, names = txgen.multisig_cases(rng, keys, forkid)
+    btxs, bjobs = txgen.std_block(rng, 40, keys, forkid=forkid, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
+    raw = [sh.tx_serialize(t) for t in btxs + mtxs]
+    jobs = bjobs + [(t + len(btxs), i, p, v) for (t, i, p, v) in mjobs]
+    labels = ["single"] * len(bjobs) + names
+    order = list(range(len(jobs)))
+    rng.shuffle(order)
+    jobs = [jobs[k] for k in order]
+    labels = [labels[k] for k in order]
+    want = _ms_oracle(coracle, raw, jobs, forkid)
+    got = hkv.verify_std_inputs(ver, raw, jobs, forkid)
+    bad = [(labels[k], got[k], want[k]) for k in range(len(jobs)) if got[k] != want[k]]
+    assert not bad, bad[:10]
+    assert _device_verify_std(torch, ver, raw, jobs, forkid) == got
+    assert all(g for g, lb in zip(got, labels) if lb == "single")
+    assert sum(got) > len(bjobs) + 40
+
+
+def test_multisig_many_inputs(torch, ver, coracle):
+    """600 P2SH 2-of-3 inputs (every third with one signature corrupted) in
+    one batch: record ranges allocated per input on device, verdicts equal
+    the oracle's."""
+    import hkv
+    rng = random.Random(4242)
+    keys = [txgen.Key(rng.randrange(1, o.N)) for _ in range(12)]
+    txs, jobs = [], []
+    for t in range(600):
+        ks = rng.sample(keys, 3)
+        script = txgen.multisig_script(2, [k.pub for k in ks])
+        tx = sh.Tx(2, [sh.TxIn(txgen.rand_script(rng, 32), 0, b"", 0xFFFFFFFF)],
+                   [sh.TxOut(1000 + t, sh.p2pkh_script(txgen.rand_script(rng, 20)))], [[]], 0)
+        msg = sh.sighash_legacy(tx, script, 5000, 0, 1)
+        idx = sorted(rng.sample(range(3), 2))
+        items = []
+        for k in idx:
+            r, s = txgen.sign(msg, ks[k].d if (t % 3 or k != idx[1]) else ks[k].d + 1, rng.randrange(1, o.N))
+            items.append(sh.der_encode(r, s) + b"\x01")
+        tx.inputs[0].script = b"\x00" + b"".join(txgen.push(x) for x in items) + txgen.push(script)
+        txs.append(sh.tx_serialize(tx))
+        jobs.append((t, 0, txgen.p2sh_script(script), 5000))
+    got = hkv.verify_std_inputs(ver, txs, jobs)
+    assert got == _ms_oracle(coracle, txs, jobs, None)
+    assert got == [t % 3 != 0 for t in range(600)]

@@ -22,7 +22,7 @@ import pytest
 import secp256k1_oracle as o
 import sighash_oracle as sh
 import txgen
-from conftest import GOLDEN
+from conftest import GOLDEN, oracle_batch
 
 
 @pytest.fixture(scope="module")
@@ -189,3 +189,52 @@ def test_p2sh_p2wpkh_rules():
     assert sh.std_input(nm, i, prev, val).ok
     assert not sh.std_input(tx, i, prev[:-1] + b"\x88", val).ok
 
+
+
+MS_VALID = {"valid", "empty_skip_ok", "mixed_sighash"}
+
+
+def multisig_verdicts(coracle, txs, jobs, forkid):
+    """Oracle verdicts of multisig (or any standard) inputs: candidate records
+    checked by the C restatement in HASKOIN mode, keys by pubkey_parse."""
+    out = []
+    for (t, i, prev, val) in jobs:
+        out.append(sh.verify_std_input(txs[t], i, prev, val, forkid,
+                                       lambda recs: oracle_batch(coracle, b"".join(recs), 1),
+                                       lambda k: o.pubkey_parse(k) is not None))
+    return out
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_multisig_oracle_labels(coracle, forkid):
+    """The restated countMulSig walk (haskoin-core verifyStdInput, PayMulSig
+    branch) on bare and P2SH m-of-n inputs: signatures in key order verify;
+    swapped, missing, extra (count m + 1 != m), wrong-key, high-S, unknown
+    hashtype, undecodable items (also past the n-th), a missing / non-OP_0
+    dummy, m > n, a wrong key count, an off-curve or hybrid key, a PUSHDATA1
+    key push (non-canonical, the template limit) and a wrong redeem hash all
+    fail; an empty item consumes exactly one key."""
+    rng = random.Random(77 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(24)]
+    txs, jobs, names = txgen.multisig_cases(rng, keys, forkid)
+    got = multisig_verdicts(coracle, txs, jobs, forkid)
+    want = [nm.split("-", 2)[2] in MS_VALID for nm in names]
+    bad = [(names[k], got[k]) for k in range(len(jobs)) if got[k] != want[k]]
+    assert not bad, bad[:10]
+    assert sum(want) > 40 and len(want) - sum(want) > 200
+
+
+def test_multisig_candidate_order_and_walk():
+    """Candidates are (j, k) for nonempty j < min(#sigs, n), k = j..n-1, in
+    that order; the walk consumes a key per step and a signature per match
+    or empty item."""
+    ms = sh.MultiSig(2, [b"a", b"b", b"c"], [None, (1, 1, 1), (1, 1, 1), (1, 1, 1)], [sh.ZERO32] * 3)
+    assert ms.candidates() == [(1, 1), (1, 2), (2, 2)]
+    # empty sig 0 consumes key a; sig 1 matches b; sig 2 vs c
+    assert ms.resolve([True, False, True], [True] * 3)
+    assert not ms.resolve([True, False, False], [True] * 3)
+    assert not ms.resolve([False, True, True], [True] * 3)      # sig 1 matches c: sig 2 has no key left
+    assert not ms.resolve([True, False, True], [True, False, True])
+    ms1 = sh.MultiSig(1, [b"a", b"b"], [(1, 1, 1)], [sh.ZERO32])
+    assert ms1.candidates() == [(0, 0), (0, 1)]
+    assert ms1.resolve([False, True], [True, True])

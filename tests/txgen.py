@@ -135,3 +135,116 @@ def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[i
         for j in range(nin):
             jobs.append((t, j, prevs[j], vals[j]))
     return txs, jobs
+
+
+# --- multisig (bare and P2SH) -------------------------------------------------
+
+def multisig_script(m: int, pubs: List[bytes]) -> bytes:
+    return bytes([0x50 + m]) + b"".join(push(p) for p in pubs) + bytes([0x50 + len(pubs), 0xAE])
+
+
+def p2sh_script(redeem: bytes) -> bytes:
+    return b"\xa9\x14" + sh.hash160(redeem) + b"\x87"
+
+
+def _ms_tx(rng: random.Random) -> sh.Tx:
+    ins = [sh.TxIn(rand_script(rng, 32), rng.randrange(4), b"", 0xFFFFFFFF) for _ in range(rng.choice([1, 2]))]
+    outs = [sh.TxOut(rng.randrange(1, 2**40), sh.p2pkh_script(rand_script(rng, 20))) for _ in range(2)]
+    return sh.Tx(1, ins, outs, [[] for _ in ins], rng.randrange(600000))
+
+
+OFF_CURVE = b"\x02" + (5).to_bytes(32, "big")   # x = 5: x^3 + 7 is not a square mod p
+
+
+def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = None):
+    """Bare and P2SH m-of-n inputs, valid and adversarial (one input per tx,
+    signatures made against the real scriptCode). Returns (txs, jobs, names)
+    with jobs = (tx index, input, prevout script, value); the verdict of each
+    is decided by the oracle (sighash_oracle.verify_std_input), not here."""
+    txs, jobs, names = [], [], []
+    base_sh = 0x41 if forkid is not None else 0x01
+    shapes = [(1, 1), (1, 2), (2, 2), (2, 3), (3, 5), (1, 3), (4, 7), (15, 15), (1, 16)]
+    variants = ["valid", "swap", "fewer", "extra", "wrong_key", "empty_skip_ok", "empty_skip_bad", "no_dummy",
+                "dummy_op1", "m_gt_n", "n_mismatch", "off_curve_other", "hybrid_key", "pushdata1_key",
+                "bad_redeem_hash", "mixed_sighash", "bad_der_after_n", "trailing_op", "high_s", "all_empty",
+                "unknown_hashtype", "sig_past_end"]
+    for (m, n) in shapes:
+        for p2sh in (False, True):
+            for var in variants:
+                if var in ("swap",) and m < 2:
+                    continue
+                if var in ("extra", "empty_skip_ok", "empty_skip_bad") and m == n:
+                    continue
+                if p2sh is False and var == "bad_redeem_hash":
+                    continue
+                ks = rng.sample(keys, n)
+                pubs = [k.pub for k in ks]
+                mm, nn = m, n
+                if var == "off_curve_other":
+                    pubs = pubs[:]
+                    pubs[-1] = OFF_CURVE
+                elif var == "hybrid_key":
+                    q = ks[-1].q
+                    pubs = pubs[:-1] + [bytes([6 | (q[1] & 1)]) + q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big")]
+                script = multisig_script(mm, pubs)
+                if var == "m_gt_n":
+                    script = bytes([0x50 + n + 1]) + script[1:] if n < 16 else b"\x61" + script[1:]
+                elif var == "n_mismatch":
+                    script = script[:-2] + bytes([0x50 + (n - 1 if n > 1 else 2), 0xAE])
+                elif var == "pushdata1_key":
+                    script = bytes([0x50 + m]) + b"\x4c" + bytes([len(pubs[0])]) + pubs[0] + \
+                        b"".join(push(p) for p in pubs[1:]) + bytes([0x50 + n, 0xAE])
+                prev = p2sh_script(script) if p2sh else script
+                if var == "bad_redeem_hash":
+                    prev = b"\xa9\x14" + bytes(20) + b"\x87"
+                tx = _ms_tx(rng)
+                i = rng.randrange(len(tx.inputs))
+                value = rng.randrange(1, 2**50)
+                # which keys sign, in key order
+                idx = sorted(rng.sample(range(n), m))
+                if var == "extra":
+                    idx = sorted(rng.sample(range(n), m + 1))
+                elif var == "fewer":
+                    idx = idx[:-1]
+                elif var == "empty_skip_ok":   # an empty item consumes key 0; the signers come later
+                    idx = sorted(rng.sample(range(1, n), m))
+                elif var == "empty_skip_bad":  # ... but key 0 itself signs: the empty item skips it
+                    idx = [0] + sorted(rng.sample(range(1, n), m - 1)) if m > 1 else [0]
+                shs = [base_sh] * len(idx)
+                if var == "mixed_sighash":
+                    shs = [rng.choice([1, 2, 3, 0x81, 0x82, 0x83]) | (0x40 if forkid is not None else 0)
+                           for _ in idx]
+                if var == "unknown_hashtype" and shs:
+                    shs[0] = 0x04
+                items = []
+                for k, shb in zip(idx, shs):
+                    msg = sh.sighash_legacy(tx, script, value, i, shb, forkid)
+                    d = ks[k].d
+                    if var == "wrong_key" and k == idx[-1]:
+                        d = rng.randrange(1, o.N)
+                    r, s = sign(msg, d, rng.randrange(1, o.N))
+                    if var == "high_s" and k == idx[0]:
+                        s = o.N - s
+                    items.append(sh.der_encode(r, s) + bytes([shb]))
+                if var == "swap":
+                    items[0], items[1] = items[1], items[0]
+                sig_part = b"".join(push(x) for x in items)
+                if var in ("empty_skip_ok", "empty_skip_bad"):
+                    sig_part = b"\x00" + sig_part
+                if var == "all_empty":
+                    sig_part = b"\x00" * m
+                if var == "bad_der_after_n":
+                    sig_part = sig_part + b"\x00" * (n - len(items)) + push(b"\x30\x02\x01\x01\x01")
+                if var == "sig_past_end":
+                    sig_part = sig_part + b"\x4c\x50\x30"
+                dummy = b"\x51" if var == "dummy_op1" else (b"" if var == "no_dummy" else b"\x00")
+                ss = dummy + sig_part
+                if var == "trailing_op":
+                    ss += b"\x75"   # OP_DROP: not a push, the decode fails
+                if p2sh:
+                    ss += push(script)
+                tx.inputs[i].script = ss
+                txs.append(tx)
+                jobs.append((len(txs) - 1, i, prev, value))
+                names.append(f"{'p2sh' if p2sh else 'bare'}-{m}of{n}-{var}")
+    return txs, jobs, names
