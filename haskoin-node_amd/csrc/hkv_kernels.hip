@@ -468,7 +468,9 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         fe_cmov(ty, nty, neg);
         const bool was_inf = inf;
         gej_accumulate(acc, inf, acc.z, tx, ty, take);
-        gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
+        // only the first nonzero digit of a lane starts from infinity: skip
+        // the 24 selects in every window where no lane of the wave does
+        if (__any(take && was_inf)) gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
       }
       // G terms every fifth window (radix 2^20): slot 0 = u1_lo * G,
       // slot 1 = u1_hi * 2^128 G; entries were DMA'd into LDS before the doublings.

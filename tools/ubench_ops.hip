@@ -19,7 +19,7 @@ constexpr int CH = 8;
 struct Stamp { unsigned long long t0, t1, r0, r1; };
 
 // instructions per chain step for each op
-static const int NINSTR[] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 3};
+static const int NINSTR[] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 3, 1, 1};
 static const char* NAMES[] = {
     "v_add_u32",                        // 0
     "v_add_co_u32_e64 (sdst)",          // 1
@@ -53,6 +53,8 @@ static const char* NAMES[] = {
     "v_lshrrev_b32_e32",                // 29
     "v_mul_lo_u32",                     // 30
     "mad(co->vcc)+addc_e32, 1 instr apart, no nop",  // 31
+    "v_cndmask_b32_e32 (vcc from v_cmp_e32 each 8)",  // 32
+    "v_cndmask_b32_e64 (s pair from v_cmp_e64 each 8)",  // 33
 };
 
 template <int OP>
@@ -77,7 +79,7 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
           case 3: asm volatile("v_add_co_u32_e64 %0, s[26:27], %0, %1" : "+v"(a[k]) : "v"(b) : "s26", "s27"); break;
           case 4: asm volatile("v_add_co_u32_e64 %0, s[28:29], %0, %1" : "+v"(a[k]) : "v"(b) : "s28", "s29"); break;
           case 5: asm volatile("v_add_co_u32_e64 %0, s[30:31], %0, %1" : "+v"(a[k]) : "v"(b) : "s30", "s31"); break;
-          case 6: asm volatile("v_add_co_u32_e64 %0, s[32:33], %0, %1" : "+v"(a[k]) : "v"(b) : "s32", "s33"); break;
+          case 6: asm volatile("v_add_co_u32_e64 %0, s[56:57], %0, %1" : "+v"(a[k]) : "v"(b) : "s56", "s57"); break;
           case 7: asm volatile("v_add_co_u32_e64 %0, s[34:35], %0, %1" : "+v"(a[k]) : "v"(b) : "s34", "s35"); break;
         }
       } else if constexpr (OP == 2) {
@@ -88,7 +90,7 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
           case 3: asm volatile("v_addc_co_u32_e64 %0, s[26:27], %0, %1, s[26:27]" : "+v"(a[k]) : "v"(b) : "s26", "s27"); break;
           case 4: asm volatile("v_addc_co_u32_e64 %0, s[28:29], %0, %1, s[28:29]" : "+v"(a[k]) : "v"(b) : "s28", "s29"); break;
           case 5: asm volatile("v_addc_co_u32_e64 %0, s[30:31], %0, %1, s[30:31]" : "+v"(a[k]) : "v"(b) : "s30", "s31"); break;
-          case 6: asm volatile("v_addc_co_u32_e64 %0, s[32:33], %0, %1, s[32:33]" : "+v"(a[k]) : "v"(b) : "s32", "s33"); break;
+          case 6: asm volatile("v_addc_co_u32_e64 %0, s[56:57], %0, %1, s[56:57]" : "+v"(a[k]) : "v"(b) : "s56", "s57"); break;
           case 7: asm volatile("v_addc_co_u32_e64 %0, s[34:35], %0, %1, s[34:35]" : "+v"(a[k]) : "v"(b) : "s34", "s35"); break;
         }
       } else if constexpr (OP == 3) {
@@ -99,7 +101,7 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
           case 3: asm volatile("v_mad_u64_u32 %0, s[26:27], %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b) : "s26", "s27"); break;
           case 4: asm volatile("v_mad_u64_u32 %0, s[28:29], %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b) : "s28", "s29"); break;
           case 5: asm volatile("v_mad_u64_u32 %0, s[30:31], %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b) : "s30", "s31"); break;
-          case 6: asm volatile("v_mad_u64_u32 %0, s[32:33], %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b) : "s32", "s33"); break;
+          case 6: asm volatile("v_mad_u64_u32 %0, s[56:57], %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b) : "s56", "s57"); break;
           case 7: asm volatile("v_mad_u64_u32 %0, s[34:35], %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b) : "s34", "s35"); break;
         }
       } else if constexpr (OP == 4) {
@@ -110,7 +112,7 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
           case 3: asm volatile("v_mad_u64_u32 %0, s[26:27], %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[26:27], %1, 0, s[26:27]" : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "s26", "s27"); break;
           case 4: asm volatile("v_mad_u64_u32 %0, s[28:29], %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[28:29], %1, 0, s[28:29]" : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "s28", "s29"); break;
           case 5: asm volatile("v_mad_u64_u32 %0, s[30:31], %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[30:31], %1, 0, s[30:31]" : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "s30", "s31"); break;
-          case 6: asm volatile("v_mad_u64_u32 %0, s[32:33], %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[32:33], %1, 0, s[32:33]" : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "s32", "s33"); break;
+          case 6: asm volatile("v_mad_u64_u32 %0, s[56:57], %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[56:57], %1, 0, s[56:57]" : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "s56", "s57"); break;
           case 7: asm volatile("v_mad_u64_u32 %0, s[34:35], %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[34:35], %1, 0, s[34:35]" : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "s34", "s35"); break;
         }
       } else if constexpr (OP == 5) {
@@ -143,7 +145,7 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
           case 3: asm volatile("v_add_co_u32_e64 %0, s[26:27], %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[26:27], %1, 0, s[26:27]" : "+v"(a[k]), "+v"(h[k]) : "v"(b) : "s26", "s27"); break;
           case 4: asm volatile("v_add_co_u32_e64 %0, s[28:29], %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[28:29], %1, 0, s[28:29]" : "+v"(a[k]), "+v"(h[k]) : "v"(b) : "s28", "s29"); break;
           case 5: asm volatile("v_add_co_u32_e64 %0, s[30:31], %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[30:31], %1, 0, s[30:31]" : "+v"(a[k]), "+v"(h[k]) : "v"(b) : "s30", "s31"); break;
-          case 6: asm volatile("v_add_co_u32_e64 %0, s[32:33], %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[32:33], %1, 0, s[32:33]" : "+v"(a[k]), "+v"(h[k]) : "v"(b) : "s32", "s33"); break;
+          case 6: asm volatile("v_add_co_u32_e64 %0, s[56:57], %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[56:57], %1, 0, s[56:57]" : "+v"(a[k]), "+v"(h[k]) : "v"(b) : "s56", "s57"); break;
           case 7: asm volatile("v_add_co_u32_e64 %0, s[34:35], %0, %2\n\ts_nop 1\n\tv_addc_co_u32_e64 %1, s[34:35], %1, 0, s[34:35]" : "+v"(a[k]), "+v"(h[k]) : "v"(b) : "s34", "s35"); break;
         }
       } else if constexpr (OP == 16) {
@@ -182,6 +184,12 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
         // with pair k's independent add in between)
         asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_add_u32_e32 %1, %1, %3\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
                      : "+v"(acc[k]), "+v"(h[k]) : "v"(a[k]), "v"(b) : "vcc");
+      } else if constexpr (OP == 32) {
+        if (k == 0) asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1" : : "v"(a[7]), "v"(b) : "vcc");
+        asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[k]) : "v"(h[k]));
+      } else if constexpr (OP == 33) {
+        if (k == 0) asm volatile("v_cmp_gt_u32_e64 s[20:21], %0, %1" : : "v"(a[7]), "v"(b) : "s20", "s21");
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a[k]) : "v"(h[k]));
       }
     }
   }
@@ -235,7 +243,7 @@ int main() {
   rc |= run<15>(n_cu); rc |= run<16>(n_cu); rc |= run<17>(n_cu); rc |= run<18>(n_cu); rc |= run<19>(n_cu);
   rc |= run<20>(n_cu); rc |= run<21>(n_cu); rc |= run<22>(n_cu); rc |= run<23>(n_cu); rc |= run<24>(n_cu);
   rc |= run<25>(n_cu); rc |= run<26>(n_cu); rc |= run<27>(n_cu); rc |= run<28>(n_cu); rc |= run<29>(n_cu);
-  rc |= run<30>(n_cu); rc |= run<31>(n_cu);
+  rc |= run<30>(n_cu); rc |= run<31>(n_cu); rc |= run<32>(n_cu); rc |= run<33>(n_cu);
   return rc;
 }
 
