@@ -133,17 +133,22 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
     for (auto& x : e) HKV_TRY(hipEventCreate(&x), "hipEventCreate");
     HKV_TRY(hipEventRecord(e[0], st), "hipEventRecord");
   }
-  HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
-  if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   // a batch of at most half a wave per SIMD (an eighth of the resident grid)
   // runs two lanes per signature (hkv_ecmult_kernel<true>): a ~24% shorter
   // dependency chain where latency, not issue, bounds the launch. Above that
   // the duplicated doublings cost more than the chain saves (measured: a
-  // 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms unsplit).
+  // 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms unsplit). The
+  // same batches run the one-launch prologue (key sqrt beside s^-1 + GLV).
 #ifndef HKV_SPLIT_DIV
 #define HKV_SPLIT_DIV 8  // split when n_pad <= resident grid / HKV_SPLIT_DIV
 #endif
+#ifndef HKV_PROLOGUE_SPLIT
+#define HKV_PROLOGUE_SPLIT 1
+#endif
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
+  HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
+          "prologue launch");
+  if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, d.bits, split,

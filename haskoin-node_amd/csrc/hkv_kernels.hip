@@ -289,6 +289,87 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 }
 
 // ---------------------------------------------------------------------------
+// 1d. small batches (the split ecmult's range, e.g. one block): prologue,
+//     s^-1 and GLV in one launch, the two independent dependency chains side
+//     by side instead of three consecutive kernels. A workgroup takes 128
+//     signatures: waves 0-1 parse the key (the 253S + 13M sqrt), waves 2-3
+//     parse the signature and run s^-1 (safegcd, one per signature: there is
+//     nothing worth batching at this size), u1 = m/s, u2 = r/s, the GLV split
+//     and the Booth recoding. Same intermediate as the three-kernel path.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* __restrict__ recs, uint32_t n,
+                                                                uint32_t n_pad, uint32_t mode,
+                                                                uint32_t* __restrict__ im) {
+  __shared__ uint32_t pk_ok_s[WG / 2];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = wv >> 1;  // wave-uniform
+  const uint32_t sub = threadIdx.x & (WG / 2 - 1);
+  const uint32_t i = blockIdx.x * (WG / 2) + sub;  // < n_pad (n_pad % WG == 0)
+  uint32_t w[REC_WORDS];
+#pragma unroll
+  for (int k = 0; k < REC_WORDS; ++k) w[k] = 0;
+  bool ok = false, glv_ok = false, n1 = false, n2 = false;
+  if (half == 0) {
+    if (i < n) {
+#pragma unroll
+      for (int k = 24; k < 42; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
+    }
+    fe x, y;
+    const bool pk = pubkey_parse_rec(w, x, y) && i < n;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      im[(size_t)(IM_QX + k) * n_pad + i] = x.v[k];
+      im[(size_t)(IM_QY + k) * n_pad + i] = y.v[k];
+    }
+    pk_ok_s[sub] = pk ? 1u : 0u;
+  } else {
+    if (i < n) {
+#pragma unroll
+      for (int k = 0; k < 24; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
+    }
+    sc r, s, m;
+    rec_be256(r.v, w, 32);
+    rec_be256(s.v, w, 64);
+    rec_be256(m.v, w, 0);
+    ok = (i < n) && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
+    const bool high = sc_is_high(s);
+    if (mode == HKV_MODE_HASKOIN) {
+      sc ns;
+      sc_neg(ns, s);
+      if (high) s = ns;  // secp256k1_ecdsa_signature_normalize
+    } else {
+      ok = ok && !high;  // secp256k1_ecdsa_verify rejects high-S
+    }
+    ok = ok && !u256_is_zero(r.v) && !u256_is_zero(s.v);
+    sc_cond_sub_n(m.v);  // m = msg32 mod n
+    if (!ok) sc_set_u32(s, 1);
+    sc sinv, u1, u2;
+    sc_inv(sinv, s);
+    sc_mul(u1, m, sinv);
+    sc_mul(u2, r, sinv);
+    uint32_t k1[5], k2[5];
+    glv_ok = glv_split(u2, k1, n1, k2, n2);
+    const bool use = ok && glv_ok;
+    uint32_t S1[5], S2[5], SL[4], SH[4];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
+    write_digits(im, n_pad, i, S1, S2, SL, SH);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
+  }
+  __syncthreads();
+  if (half == 1) {
+    // flags as the three-kernel path leaves them (hkv_glv_kernel)
+    uint32_t f = (ok && pk_ok_s[sub]) ? FLAG_VALID : 0u;
+    f |= (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
+    if (!glv_ok) f &= ~FLAG_VALID;
+    im[(size_t)IM_FLAGS * n_pad + i] = f;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 2. ecmult + x compare
 // ---------------------------------------------------------------------------
 // Per-lane Q table, entry-major then lane: entry e of lane L is 96 contiguous
@@ -888,8 +969,13 @@ namespace hkv {
 
 static inline uint32_t ceil_div(size_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
-hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im,
+hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im, bool split,
                            hipStream_t st) {
+  if (split) {  // n_pad % WG == 0: n_pad / 128 workgroups of 128 signatures
+    hipLaunchKernelGGL(hkv_prologue_split_kernel, dim3(n_pad / (WG / 2)), dim3(WG), 0, st, (const uint32_t*)recs, n,
+                       n_pad, mode, im);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(hkv_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st,
                      (const uint32_t*)recs, n, n_pad, mode, im);
   hipError_t e = hipGetLastError();
