@@ -375,14 +375,82 @@ HKV_DEV uint32_t gen_next(Gen& g) {
   return b;
 }
 
+#ifndef HKV_STREAM_WORDS
+#define HKV_STREAM_WORDS 1
+#endif
+
+// The next up to 4 message bytes, packed big-endian from the top of w;
+// returns how many (fewer than 4 only at the end of the message). Inside a
+// piece the 4 bytes come from 4 independent loads (or the literal's next
+// 32 bits) instead of 4 dependent load / store rounds; piece boundaries take
+// the byte path.
+HKV_DEV uint32_t gen_word(Gen& g, uint32_t& w) {
+  if (g.rem >= 4u) {
+    if (g.src) {
+      const uint8_t* s = g.src;
+      w = ((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) | ((uint32_t)s[2] << 8) | (uint32_t)s[3];
+      g.src += 4;
+    } else {
+      w = __builtin_bswap32((uint32_t)g.lit);
+      g.lit >>= 32;
+    }
+    g.rem -= 4u;
+    return 4u;
+  }
+  uint32_t n = 0;
+  w = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (!gen_more(g)) break;
+    w |= gen_next(g) << (24 - 8 * k);
+    ++n;
+  }
+  return n;
+}
+
 // SHA-256 of the generator's message, block-synchronous over the wave: each
 // iteration every live lane writes its next 64 bytes (message, then 0x80,
 // zeros and the 64-bit length) into its LDS slot buf[word * WG + tid] and all
 // of them compress together. Call from wave-uniform control flow.
 HKV_DEV void sha256_stream(uint32_t h[8], Gen& g, bool live, uint32_t* buf) {
   sha256_init(h);
-  uint8_t* bb = reinterpret_cast<uint8_t*>(buf);
   const uint32_t tid = threadIdx.x;
+#if HKV_STREAM_WORDS
+  // word at a time: 16 LDS word stores per block; 0x80 right after the last
+  // message byte; the length in words 14-15 of the block that has room
+  uint32_t st = live ? 0u : 3u;  // 0 message, 1 padding (0x80 written), 3 done
+  uint64_t len = 0;
+  while (__any(st != 3u)) {
+    if (st != 3u) {
+      bool fits = st == 1u;  // a block after the 0x80 block always has room
+#pragma unroll 1
+      for (uint32_t k = 0; k < 16u; ++k) {
+        uint32_t v = 0;
+        if (st == 0u) {
+          const uint32_t nb = gen_word(g, v);
+          len += nb;
+          if (nb < 4u) {
+            v |= 0x80u << (24 - 8 * nb);
+            st = 1u;
+            fits = k < 14u;
+          }
+        }
+        buf[k * WG + tid] = v;
+      }
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = buf[k * WG + tid];
+      const bool last = st == 1u && fits;
+      if (last) {
+        const uint64_t bits = len << 3;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+      }
+      sha256_compress(h, w);
+      if (last) st = 3u;
+    }
+  }
+#else
+  uint8_t* bb = reinterpret_cast<uint8_t*>(buf);
   uint32_t st = live ? 0u : 3u;  // 0 message, 1 padding, 2 last block, 3 done
   uint64_t len = 0;
   bool pad_ok = false;
@@ -416,6 +484,7 @@ HKV_DEV void sha256_stream(uint32_t h[8], Gen& g, bool live, uint32_t* buf) {
       if (st == 2u) st = 3u;
     }
   }
+#endif
 }
 
 // SHA-256d digest -> 8 words in digest byte order
