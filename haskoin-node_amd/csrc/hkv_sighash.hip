@@ -864,6 +864,36 @@ HKV_DEV bool read_push(const uint8_t* p, uint32_t& off, uint32_t end, uint32_t& 
   return true;
 }
 
+// haskoin PubKeyI encoding: 02/03 + 32 bytes or 04 + 64 bytes
+HKV_DEV bool pubkey_bytes_ok(const uint8_t* p, uint32_t len) {
+  return (len == 33u && (p[0] == 2u || p[0] == 3u)) || (len == 65u && p[0] == 4u);
+}
+// direct-push P2PK script (21 <33> ac / 41 <65> ac)
+HKV_DEV bool is_p2pk(const uint8_t* sc, uint32_t L) {
+  return ((L == 35u && sc[0] == 0x21u) || (L == 67u && sc[0] == 0x41u)) && sc[L - 1] == 0xACu;
+}
+HKV_DEV bool is_p2pkh(const uint8_t* sc, uint32_t L) {
+  return L == 25u && sc[0] == 0x76u && sc[1] == 0xA9u && sc[2] == 0x14u && sc[23] == 0x88u && sc[24] == 0xACu;
+}
+// 20-byte hash in memory == RIPEMD-160 words / 32-byte hash == SHA-256 state
+HKV_DEV bool eq_h160(const uint8_t* p, const uint32_t rip[5]) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    ok = ok && (uint32_t)(p[4 * k] | (p[4 * k + 1] << 8) | (p[4 * k + 2] << 16) | ((uint32_t)p[4 * k + 3] << 24)) == rip[k];
+  return ok;
+}
+HKV_DEV bool eq_sha256(const uint8_t* p, const uint32_t h[8]) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    ok = ok && (((uint32_t)p[4 * k] << 24) | (p[4 * k + 1] << 16) | (p[4 * k + 2] << 8) | p[4 * k + 3]) == h[k];
+  return ok;
+}
+
+// Single-signature templates (haskoin verifyStdInput): P2PK, P2PKH, P2WPKH;
+// P2SH around P2PK / P2PKH / P2WPKH / P2WSH; P2WSH (native or P2SH-nested)
+// around P2PK / P2PKH. Multisig inputs: hkv_ms_* (section 4).
 __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
                                                            const uint32_t* __restrict__ txt,
                                                            const uint8_t* __restrict__ scripts, uint32_t scripts_len,
@@ -873,13 +903,22 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   const bool in_range = jx < n;
   bool ok = false;
-  uint32_t kind = 0;  // 1 P2PK, 2 P2PKH, 3 P2WPKH, 4 P2SH-P2WPKH
   const uint32_t* row = txt;
   const uint8_t* spk = scripts;
-  uint32_t sig_off = 0, sig_len = 0, pub_off = 0, pub_len = 0, sh = 0, input = 0;
+  uint32_t sig_off = 0, sig_len = 0, pub_len = 0, sh = 0, input = 0;
   const uint8_t* pub = txs;
-  const uint8_t* prog = scripts;  // the 20-byte witness program (kinds 3, 4)
   uint64_t value = 0;
+  // what the checks and the sighash need
+  const uint8_t* code = scripts;  // sighash scriptCode (P2WPKH form: the 20-byte program)
+  uint32_t code_len = 0;
+  bool segwit = false, p2wpkh = false;
+  const uint8_t* kh = scripts;    // HASH160(pubkey) must equal these 20 bytes (has_kh)
+  const uint8_t* rd = txs;        // P2SH: HASH160(redeem script) == spk[2..22] (has_rd)
+  uint32_t rd_len = 0;
+  const uint8_t* ws = txs;        // P2WSH: SHA-256(witness script) == wprog (has_ws)
+  uint32_t ws_len = 0;
+  const uint8_t* wprog = scripts;
+  bool has_kh = false, has_rd = false, has_ws = false;
   uint32_t r[8], s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) r[k] = s[k] = 0;
@@ -895,103 +934,170 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
     if (ok) {
       spk = scripts + jb.script_off;
       const uint32_t L = jb.script_len;
-      if ((L == 35 && spk[0] == 0x21u && spk[34] == 0xACu) || (L == 67 && spk[0] == 0x41u && spk[66] == 0xACu))
-        kind = 1;
-      else if (L == 25 && spk[0] == 0x76u && spk[1] == 0xA9u && spk[2] == 0x14u && spk[23] == 0x88u &&
-               spk[24] == 0xACu)
-        kind = 2;
-      else if (L == 22 && spk[0] == 0x00u && spk[1] == 0x14u)
-        kind = 3;
-      else if (L == 23 && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u)
-        kind = 4;
-      ok = kind != 0;
-    }
-    if (ok) {
       uint32_t in_off, ss_off, ss_len, seq_off;
       walk_input(txs, row[TXT_INS], jb.input, in_off, ss_off, ss_len, seq_off);
       const uint32_t ss_end = ss_off + ss_len;
-      uint32_t c = ss_off;
-      if (kind == 1) {  // scriptSig = <sig>; pubkey from the prevout
+      uint32_t c = ss_off, pub_off = 0;
+      // witness program to open: 1 P2WPKH [sig, pub], 2 P2WSH [stack.., ws]
+      uint32_t open_wit = 0;
+      if (is_p2pk(spk, L)) {  // scriptSig = <sig>; pubkey from the prevout
         ok = read_push(txs, c, ss_end, sig_off, sig_len) && c == ss_end;
         pub = spk + 1;
-        pub_len = jb.script_len - 2;
-      } else if (kind == 2) {  // scriptSig = <sig> <pubkey>
+        pub_len = L - 2;
+        code = spk;
+        code_len = L;
+      } else if (is_p2pkh(spk, L)) {  // scriptSig = <sig> <pubkey>
         ok = read_push(txs, c, ss_end, sig_off, sig_len) && read_push(txs, c, ss_end, pub_off, pub_len) &&
              c == ss_end;
         pub = txs + pub_off;
-      } else {  // witness = [sig, pubkey]; P2WPKH: empty scriptSig,
-                // P2SH-P2WPKH: scriptSig = one push of the redeem script 00 14 <h20>
-        if (kind == 3) {
-          ok = ss_len == 0;
-          prog = spk + 2;
-        } else {
-          uint32_t rd_off = 0, rd_len = 0;
-          ok = read_push(txs, c, ss_end, rd_off, rd_len) && c == ss_end && rd_len == 22u && txs[rd_off] == 0u &&
-               txs[rd_off + 1] == 0x14u;
-          prog = txs + rd_off + 2;
+        kh = spk + 3;
+        has_kh = true;
+        code = spk;
+        code_len = 25;
+      } else if (L == 22u && spk[0] == 0x00u && spk[1] == 0x14u) {  // P2WPKH: empty scriptSig
+        ok = ss_len == 0;
+        code = kh = spk + 2;
+        has_kh = true;
+        open_wit = 1;
+      } else if (L == 34u && spk[0] == 0x00u && spk[1] == 0x20u) {  // P2WSH: empty scriptSig
+        ok = ss_len == 0;
+        wprog = spk + 2;
+        open_wit = 2;
+      } else if (L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u) {
+        // P2SH: every op a push; the last one is the redeem script
+        uint32_t np = 0, o0 = 0, l0 = 0, o1 = 0, l1 = 0, ol = 0, ll = 0;
+        while (ok && c < ss_end) {
+          uint32_t d_off = 0, d_len = 0;
+          ok = read_push(txs, c, ss_end, d_off, d_len);
+          if (np == 0) { o0 = d_off; l0 = d_len; }
+          if (np == 1) { o1 = d_off; l1 = d_len; }
+          ol = d_off;
+          ll = d_len;
+          ++np;
         }
-        ok = ok && (row[TXT_FLAGS] & TXF_WITNESS);
+        ok = ok && np >= 1;
+        rd = txs + ol;
+        rd_len = ll;
+        has_rd = true;
         if (ok) {
-          uint32_t w = walk_witness(txs, row[TXT_OUTS_END], jb.input);
-          ok = get_varint(txs, w) == 2u;
+          if (ll == 22u && rd[0] == 0u && rd[1] == 0x14u) {  // P2SH-P2WPKH
+            ok = np == 1;
+            code = kh = rd + 2;
+            has_kh = true;
+            open_wit = 1;
+          } else if (ll == 34u && rd[0] == 0u && rd[1] == 0x20u) {  // P2SH-P2WSH
+            ok = np == 1;
+            wprog = rd + 2;
+            open_wit = 2;
+          } else if (is_p2pk(rd, ll)) {  // P2SH-P2PK: <sig> <redeem>
+            ok = np == 2;
+            sig_off = o0; sig_len = l0;
+            pub = rd + 1;
+            pub_len = ll - 2;
+            code = rd;
+            code_len = ll;
+          } else if (is_p2pkh(rd, ll)) {  // P2SH-P2PKH: <sig> <pubkey> <redeem>
+            ok = np == 3;
+            sig_off = o0; sig_len = l0;
+            pub = txs + o1;
+            pub_len = l1;
+            kh = rd + 3;
+            has_kh = true;
+            code = rd;
+            code_len = 25;
+          } else {
+            ok = false;  // multisig redeem scripts: hkv_ms_*; anything else is not standard
+          }
+        }
+      } else {
+        ok = false;
+      }
+      if (ok && open_wit) {
+        ok = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
+        uint32_t w = ok ? walk_witness(txs, row[TXT_OUTS_END], jb.input) : 0u;
+        const uint32_t cnt = ok ? get_varint(txs, w) : 0u;
+        if (open_wit == 1) {  // [sig, pubkey]
+          ok = ok && cnt == 2u;
           if (ok) {
             sig_len = get_varint(txs, w);
             sig_off = w;
             w += sig_len;
             pub_len = get_varint(txs, w);
-            pub_off = w;
-            pub = txs + pub_off;
+            pub = txs + w;
           }
+          segwit = p2wpkh = true;
+        } else {  // [sig, ws] (P2PK) or [sig, pubkey, ws] (P2PKH)
+          ok = ok && (cnt == 2u || cnt == 3u);
+          if (ok) {
+            sig_len = get_varint(txs, w);
+            sig_off = w;
+            w += sig_len;
+            uint32_t l1 = 0, o1 = 0;
+            if (cnt == 3u) {
+              l1 = get_varint(txs, w);
+              o1 = w;
+              w += l1;
+            }
+            ws_len = get_varint(txs, w);
+            ws = txs + w;
+            has_ws = true;
+            if (cnt == 2u && is_p2pk(ws, ws_len)) {
+              pub = ws + 1;
+              pub_len = ws_len - 2;
+            } else if (cnt == 3u && is_p2pkh(ws, ws_len)) {
+              pub = txs + o1;
+              pub_len = l1;
+              kh = ws + 3;
+              has_kh = true;
+            } else {
+              ok = false;  // P2WSH multisig: hkv_ms_*
+            }
+            code = ws;
+            code_len = ws_len;
+          }
+          segwit = true;
         }
       }
     }
     if (ok) ok = decode_tx_sig(txs, sig_off, sig_len, forkid, r, s, sh);
-    // haskoin PubKeyI encoding
-    if (ok) ok = (pub_len == 33 && (pub[0] == 2u || pub[0] == 3u)) || (pub_len == 65 && pub[0] == 4u);
+    if (ok) ok = pubkey_bytes_ok(pub, pub_len);
   }
-  // HASH160(pubkey) == program / key hash (P2PKH, P2WPKH)
-  const bool need_h160 = ok && kind != 1;
   Gen g;
   uint32_t h[8], d[8];
+  // HASH160(pubkey) == the key hash (P2PKH, P2WPKH and their wrapped forms)
+  const bool need_h160 = ok && has_kh;
   if (__any(need_h160)) {
     gen_clear(g);
     g.code = pub; g.code_len = pub_len; g.phase = PH_RANGE;
     sha256_stream(h, g, need_h160, buf);
     uint32_t rip[5];
     ripemd160_of_digest(rip, h);
-    if (need_h160) {
-      const uint8_t* hp20 = kind == 2 ? spk + 3 : (kind == 1 ? spk : prog);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const uint32_t want = hp20[4 * k] | (hp20[4 * k + 1] << 8) | (hp20[4 * k + 2] << 16) |
-                              ((uint32_t)hp20[4 * k + 3] << 24);
-        ok = ok && want == rip[k];
-      }
-    }
+    if (need_h160) ok = ok && eq_h160(kh, rip);
   }
-  // P2SH-P2WPKH: HASH160(redeem script 00 14 <program>) == the P2SH hash
-  const bool need_rd = ok && kind == 4;
+  // P2SH: HASH160(redeem script) == the script hash
+  const bool need_rd = ok && has_rd;
   if (__any(need_rd)) {
     gen_clear(g);
-    g.code = prog - 2; g.code_len = 22; g.phase = PH_RANGE;
+    g.code = rd; g.code_len = rd_len; g.phase = PH_RANGE;
     sha256_stream(h, g, need_rd, buf);
     uint32_t rip[5];
     ripemd160_of_digest(rip, h);
-    if (need_rd) {
-      const uint8_t* hp20 = spk + 2;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const uint32_t want = hp20[4 * k] | (hp20[4 * k + 1] << 8) | (hp20[4 * k + 2] << 16) |
-                              ((uint32_t)hp20[4 * k + 3] << 24);
-        ok = ok && want == rip[k];
-      }
-    }
+    if (need_rd) ok = ok && eq_h160(spk + 2, rip);
   }
-  // sighash: P2PK / P2PKH -> txSigHash with scriptCode = prevout script;
-  // P2WPKH -> txSigHashForkId with scriptCode = 76 a9 14 <h20> 88 ac
+  // P2WSH: SHA-256(witness script) == the 32-byte program
+  const bool need_ws = ok && has_ws;
+  if (__any(need_ws)) {
+    gen_clear(g);
+    g.code = ws; g.code_len = ws_len; g.phase = PH_RANGE;
+    sha256_stream(h, g, need_ws, buf);
+    if (need_ws) ok = ok && eq_sha256(wprog, h);
+  }
+  // sighash: legacy txSigHash over the scriptCode (prevout or redeem script),
+  // or txSigHashForkId (BIP143) over 76 a9 14 <h20> 88 ac (P2WPKH) / the
+  // witness script (P2WSH)
   JobCtx c;
   c.forkid_form = false; c.one = false; c.single_hash = false;
-  if (ok) job_setup(c, txs, row, input, sh, kind >= 3, forkid);
+  if (ok) job_setup(c, txs, row, input, sh, segwit, forkid);
   uint8_t* rec = recs + (size_t)jx * REC_SIZE;
   uint32_t* r32 = reinterpret_cast<uint32_t*>(rec);
   const bool need_single = ok && c.single_hash;
@@ -1007,8 +1113,7 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   }
   const bool live = ok && !c.one;
   if (!live) gen_clear(g);
-  else if (kind >= 3) gen_job(g, c, txs, row, prog, 20, true, value, r32);
-  else gen_job(g, c, txs, row, spk, kind == 1 ? (pub_len + 2) : 25u, false, value, r32);
+  else gen_job(g, c, txs, row, code, p2wpkh ? 20u : code_len, p2wpkh, value, r32);
   sha256_stream(h, g, live, buf);
   sha256d_finish(d, h);
   if (!in_range) return;
@@ -1093,55 +1198,105 @@ HKV_DEV bool skip_op(const uint8_t* p, uint32_t& off, uint32_t end) {
 }
 
 struct MsIn {
-  const uint8_t* code;  // scriptCode: the prevout script (bare) or the redeem script (P2SH)
+  const uint8_t* code;  // scriptCode: the prevout, redeem or witness script
   uint32_t code_len;
-  uint32_t it_off, it_end;  // the signature items (after the OP_0 dummy, before the redeem push)
+  // the signature items: scriptSig form — the byte range after the OP_0
+  // dummy (and before a P2SH redeem push); witness form — it_off is the
+  // length varint of the item after the empty dummy, n_items of them
+  uint32_t it_off, it_end, n_items;
   uint32_t m, n, s_eff, mask, n_cand;
-  bool p2sh;
+  bool p2sh, wit;            // HASH160(rd) == the P2SH hash; witness form (SHA-256 check, BIP143)
+  const uint8_t* rd;         // P2SH: the pushed redeem script (a multisig script, or 00 20 <h32>)
+  uint32_t rd_len;
+  const uint8_t* wprog;      // witness form: the 32-byte program
 };
 
-// decode a multisig input except the P2SH redeem HASH160 (needs SHA-256)
+// next item: d_len == 0 means TxSignatureEmpty; false = not a push (decode fails)
+HKV_DEV bool ms_item(const uint8_t* txs, const MsIn& r, uint32_t& off, uint32_t& d_off, uint32_t& d_len) {
+  if (r.wit) {
+    d_len = get_varint(txs, off);
+    d_off = off;
+    off += d_len;
+    return true;
+  }
+  if (txs[off] == 0u) {
+    ++off;
+    d_len = 0;
+    return true;
+  }
+  return read_push(txs, off, r.it_end, d_off, d_len);
+}
+
+// decode a multisig input except the hash checks (P2SH HASH160, P2WSH SHA-256)
 HKV_DEV bool ms_parse(MsIn& r, const uint8_t* txs, const uint32_t* row, uint32_t input, const uint8_t* spk,
                       uint32_t L, int32_t forkid) {
   r.p2sh = L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u;
+  r.wit = false;
+  r.rd = txs;
+  r.rd_len = 0;
+  r.wprog = spk;
   uint32_t in_off, ss_off, ss_len, seq_off;
   walk_input(txs, row[TXT_INS], input, in_off, ss_off, ss_len, seq_off);
   const uint32_t end = ss_off + ss_len;
-  if (ss_len == 0 || txs[ss_off] != 0u) return false;  // haskoin matchMulSig: OP_0 first
-  r.it_off = ss_off + 1;
-  if (r.p2sh) {
-    uint32_t off = ss_off + 1, last = 0, n_ops = 0;
-    while (off < end) {
-      last = off;
-      if (!skip_op(txs, off, end)) return false;
-      ++n_ops;
-    }
-    if (n_ops == 0) return false;
-    uint32_t c = last, d_off = 0, d_len = 0;
-    if (!read_push(txs, c, end, d_off, d_len)) return false;  // the redeem script: OP_PUSHDATA
-    r.code = txs + d_off;
-    r.code_len = d_len;
-    r.it_end = last;
+  if (L == 34u && spk[0] == 0u && spk[1] == 0x20u) {  // P2WSH: empty scriptSig
+    if (ss_len != 0) return false;
+    r.wit = true;
+    r.wprog = spk + 2;
+  } else if (r.p2sh && ss_len > 0 && txs[ss_off] != 0u) {  // P2SH-P2WSH: exactly one push of 00 20 <h32>
+    uint32_t c = ss_off, d_off = 0, d_len = 0;
+    if (!read_push(txs, c, end, d_off, d_len) || c != end || d_len != 34u || txs[d_off] != 0u ||
+        txs[d_off + 1] != 0x20u)
+      return false;
+    r.wit = true;
+    r.rd = txs + d_off;
+    r.rd_len = 34;
+    r.wprog = r.rd + 2;
+  }
+  if (r.wit) {  // witness = [empty dummy] ++ items ++ [witness script]
+    if (!(row[TXT_FLAGS] & TXF_WITNESS)) return false;
+    uint32_t w = walk_witness(txs, row[TXT_OUTS_END], input);
+    const uint32_t cnt = get_varint(txs, w);
+    if (cnt < 2u || get_varint(txs, w) != 0u) return false;
+    r.it_off = w;
+    r.n_items = cnt - 2u;
+    for (uint32_t k = 0; k < r.n_items; ++k) w += get_varint(txs, w);
+    r.code_len = get_varint(txs, w);
+    r.code = txs + w;
+    r.it_end = w;
   } else {
-    r.code = spk;
-    r.code_len = L;
-    r.it_end = end;
+    if (ss_len == 0 || txs[ss_off] != 0u) return false;  // haskoin matchMulSig: OP_0 first
+    r.it_off = ss_off + 1;
+    if (r.p2sh) {
+      uint32_t off = ss_off + 1, last = 0, n_ops = 0;
+      while (off < end) {
+        last = off;
+        if (!skip_op(txs, off, end)) return false;
+        ++n_ops;
+      }
+      if (n_ops == 0) return false;
+      uint32_t c = last, d_off = 0, d_len = 0;
+      if (!read_push(txs, c, end, d_off, d_len)) return false;  // the redeem script: OP_PUSHDATA
+      r.code = r.rd = txs + d_off;
+      r.code_len = r.rd_len = d_len;
+      r.it_end = last;
+    } else {
+      r.code = spk;
+      r.code_len = L;
+      r.it_end = end;
+    }
+    r.n_items = 0xFFFFFFFFu;  // until it_end
   }
   if (!ms_template(r.code, r.code_len, r.m, r.n)) return false;
   uint32_t j = 0, mask = 0, cand = 0, off = r.it_off;
-  while (off < r.it_end) {
-    if (txs[off] == 0u) {
-      ++off;  // OP_0: TxSignatureEmpty
-    } else {
-      uint32_t d_off = 0, d_len = 0;
-      if (!read_push(txs, off, r.it_end, d_off, d_len)) return false;  // any other op fails the decode
-      if (d_len) {
-        uint32_t rr[8], ss[8], sh;
-        if (!decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh)) return false;
-        if (j < r.n) {
-          mask |= 1u << j;
-          cand += r.n - j;
-        }
+  while (r.wit ? j < r.n_items : off < r.it_end) {
+    uint32_t d_off = 0, d_len = 0;
+    if (!ms_item(txs, r, off, d_off, d_len)) return false;  // any other op fails the decode
+    if (d_len) {
+      uint32_t rr[8], ss[8], sh;
+      if (!decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh)) return false;
+      if (j < r.n) {
+        mask |= 1u << j;
+        cand += r.n - j;
       }
     }
     ++j;
@@ -1172,9 +1327,9 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
   __shared__ uint32_t buf[16 * WG];
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   MsIn r;
-  r.p2sh = false;
-  r.code = scripts;
-  r.code_len = 0;
+  r.p2sh = r.wit = false;
+  r.code = r.rd = r.wprog = scripts;
+  r.code_len = r.rd_len = 0;
   bool ok = false;
   const uint8_t* spk = scripts;
   if (jx < n) {
@@ -1184,31 +1339,34 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
     if (ok) {
       const uint32_t L = jb.script_len;
       const bool p2sh = L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u;
+      const bool p2wsh = L == 34u && spk[0] == 0u && spk[1] == 0x20u;
       const bool bare = L >= 3u && spk[L - 1] == 0xAEu;
-      ok = (p2sh || bare) && ms_parse(r, txs, row, jb.input, spk, L, forkid);
+      ok = (p2sh || p2wsh || bare) && ms_parse(r, txs, row, jb.input, spk, L, forkid);
     }
   }
+  Gen g;
+  uint32_t h[8];
   // P2SH: HASH160(redeem script) == the script hash
   const bool need = ok && r.p2sh;
   if (__any(need)) {
-    Gen g;
-    uint32_t h[8];
     gen_clear(g);
-    g.code = r.code;
-    g.code_len = r.code_len;
+    g.code = r.rd;
+    g.code_len = r.rd_len;
     g.phase = PH_RANGE;
     sha256_stream(h, g, need, buf);
     uint32_t rip[5];
     ripemd160_of_digest(rip, h);
-    if (need) {
-      const uint8_t* hp20 = spk + 2;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const uint32_t want = hp20[4 * k] | (hp20[4 * k + 1] << 8) | (hp20[4 * k + 2] << 16) |
-                              ((uint32_t)hp20[4 * k + 3] << 24);
-        ok = ok && want == rip[k];
-      }
-    }
+    if (need) ok = ok && eq_h160(spk + 2, rip);
+  }
+  // P2WSH (native or nested): SHA-256(witness script) == the program
+  const bool need_ws = ok && r.wit;
+  if (__any(need_ws)) {
+    gen_clear(g);
+    g.code = r.code;
+    g.code_len = r.code_len;
+    g.phase = PH_RANGE;
+    sha256_stream(h, g, need_ws, buf);
+    if (need_ws) ok = ok && eq_sha256(r.wprog, h);
   }
   if (jx < n) {
     desc[2 * (size_t)jx] = ok ? (MS_OK | (r.p2sh ? MS_P2SH : 0u) | r.m | (r.n << 8) | (r.s_eff << 16)) : 0u;
@@ -1255,7 +1413,8 @@ __global__ void __launch_bounds__(WG) hkv_ms_emit_kernel(const uint8_t* __restri
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   bool go = jx < n && (desc[2 * (size_t)jx] & MS_OK);
   MsIn r;
-  r.code = scripts; r.code_len = 0; r.s_eff = 0; r.mask = 0; r.n = 0; r.it_off = r.it_end = 0;
+  r.code = r.rd = r.wprog = scripts; r.code_len = r.rd_len = 0; r.s_eff = 0; r.mask = 0; r.n = 0;
+  r.it_off = r.it_end = 0; r.p2sh = r.wit = false;
   const uint32_t* row = txt;
   const uint8_t* spk = scripts;
   uint32_t input = 0;
@@ -1287,10 +1446,7 @@ __global__ void __launch_bounds__(WG) hkv_ms_emit_kernel(const uint8_t* __restri
   for (uint32_t j = 0; __any(go && j < r.s_eff); ++j) {
     const bool here = go && j < r.s_eff;
     uint32_t d_off = 0, d_len = 0;
-    if (here) {
-      if (txs[off] == 0u) ++off;
-      else (void)read_push(txs, off, r.it_end, d_off, d_len);
-    }
+    if (here) (void)ms_item(txs, r, off, d_off, d_len);
     const bool live = here && ((r.mask >> j) & 1u);
     uint32_t rr[8], ss[8], sh = 0;
 #pragma unroll
@@ -1298,7 +1454,7 @@ __global__ void __launch_bounds__(WG) hkv_ms_emit_kernel(const uint8_t* __restri
     if (live) (void)decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh);
     JobCtx c;
     c.forkid_form = false; c.one = false; c.single_hash = false;
-    if (live) job_setup(c, txs, row, input, sh, false, forkid);
+    if (live) job_setup(c, txs, row, input, sh, r.wit, forkid);  // P2WSH: BIP143 over the witness script
     uint32_t* r32 = reinterpret_cast<uint32_t*>(cand + (size_t)idx * REC_SIZE);  // first record of sig j
     const bool need_single = live && c.single_hash;
     if (__any(need_single)) {

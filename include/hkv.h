@@ -28,10 +28,11 @@
  *   hkv_verify_std_inputs / hkv_verify_std_inputs_device
  *       replaces N calls of haskoin-core
  *       `verifyStdInput :: Network -> Ctx -> Tx -> Int -> ScriptOutput -> Word64 -> Bool`
- *       (Haskoin.Transaction.Builder) for P2PK / P2PKH / P2WPKH /
- *       P2SH-P2WPKH and bare / P2SH multisig prevouts: decodeTxSig (strict
- *       DER, low S, hashtype), HASH160 check, sighash, verifyHashSig and the
- *       countMulSig walk, all on device.
+ *       (Haskoin.Transaction.Builder) for P2PK / P2PKH / P2WPKH / multisig
+ *       prevouts, bare or behind P2SH / P2WSH / P2SH-P2WSH: decodeTxSig
+ *       (strict DER, low S, hashtype), the HASH160 / SHA-256 script checks,
+ *       legacy or BIP143 sighash, verifyHashSig and the countMulSig walk,
+ *       all on device.
  *   hkv_check_headers / hkv_check_headers_device
  *       replaces the per-header part of haskoin-core `connectBlocks` reached
  *       from importHeaders (/root/reference/src/Haskoin/Node/Chain.hs:500-520):
@@ -168,10 +169,11 @@ typedef struct hkv_sighash_job {
 
 /* One standard input for verifyStdInput: input `input` of tx `tx` spends a
  * prevout with scriptPubKey = scripts[script_off, +script_len) and amount
- * `value`. Templates: P2PK (21 <33> ac / 41 <65> ac), P2PKH, P2WPKH,
- * P2SH-P2WPKH, bare multisig (OP_m <keys> OP_n OP_CHECKMULTISIG, keys as
- * direct 21 / 41 pushes) and P2SH multisig (the same script as the redeem
- * script); any other prevout script verifies false. 24 bytes. */
+ * `value`. Templates (haskoin verifyStdInput): P2PK (21 <33> ac / 41 <65> ac),
+ * P2PKH, P2WPKH, multisig (OP_m <keys> OP_n OP_CHECKMULTISIG, keys as direct
+ * 21 / 41 pushes), each of P2PK / P2PKH / P2WPKH / P2WSH / multisig behind
+ * P2SH, and P2PK / P2PKH / multisig behind P2WSH (native or P2SH-nested);
+ * any other prevout script verifies false. 24 bytes. */
 typedef struct hkv_input_job {
   uint32_t tx;
   uint32_t input;

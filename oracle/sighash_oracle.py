@@ -542,9 +542,10 @@ class StdInput:
 
 
 def std_input(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[int] = None) -> StdInput:
-    """The non-ECDSA half of verifyStdInput for P2PK / P2PKH / P2WPKH /
-    P2SH-P2WPKH prevouts: template match, strict signature decode, HASH160 check and
-    sighash. The input verifies iff ok and verifyHashSig(msg32, (r, s), pubkey).
+    """The non-ECDSA half of verifyStdInput for the single-signature
+    templates: P2PK, P2PKH, P2WPKH, P2SH-wrapped P2PK / P2PKH / P2WPKH,
+    P2WSH-wrapped P2PK / P2PKH (native and P2SH-nested): template match,
+    strict signature decode, HASH160 / SHA-256 script checks and sighash. The input verifies iff ok and verifyHashSig(msg32, (r, s), pubkey).
     P2PK is matched in its direct-push forms (21 <33> ac, 41 <65> ac)."""
     if i >= len(tx.inputs):
         return StdInput(False)
@@ -582,26 +583,83 @@ def std_input(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[i
         r, s, sh = ts
         m = sighash_forkid(tx, p2pkh_script(prev_script[2:22]), value, i, sh, forkid)
         return StdInput(True, m, r, s, pub)
-    if len(prev_script) == 23 and prev_script[:2] == b"\xa9\x14" and prev_script[22] == 0x87:
-        # P2SH-P2WPKH (BIP16 + BIP141): scriptSig is one push of the redeem
-        # script 00 14 <h20> whose HASH160 is the P2SH hash; then as P2WPKH.
-        # haskoin: the nested-output branch of verifyStdInput. Parity unpinned
-        # by reference data (the fixtures hold no P2SH spend).
-        items = _push_items(tx.inputs[i].script)
+    if len(prev_script) == 34 and prev_script[:2] == b"\x00\x20":
+        # P2WSH (haskoin verifySegwitInput, PayWitnessScriptHash): empty
+        # scriptSig, witness = stack ++ [witness script], SHA-256(witness
+        # script) == the program, the script a PayPK / PayPKHash (multisig:
+        # std_multisig), BIP143 sighash over the witness script.
+        if len(tx.inputs[i].script) != 0:
+            return StdInput(False)
         wit = tx.witness[i] if i < len(tx.witness) else []
-        if items is None or len(items) != 1 or len(wit) != 2:
+        return _p2wsh_single(tx, i, prev_script[2:34], wit, value, forkid)
+    if len(prev_script) == 23 and prev_script[:2] == b"\xa9\x14" and prev_script[22] == 0x87:
+        # P2SH (BIP16): the scriptSig's last push is the redeem script, whose
+        # HASH160 is the script hash. Nested segwit (haskoin's
+        # nestedScriptOutput branch): the scriptSig is exactly that push of
+        # 00 14 <h20> (P2SH-P2WPKH: then as P2WPKH of the program) or
+        # 00 20 <h32> (P2SH-P2WSH). Otherwise verifyLegacyInput on the redeem
+        # script: PayPK with [sig], PayPKHash with [sig, pub] before it, legacy
+        # sighash over the redeem script (multisig: std_multisig). No reference
+        # data holds a P2SH spend: parity unpinned.
+        items = _push_items(tx.inputs[i].script)
+        if items is None or not items or hash160(items[-1]) != prev_script[2:22]:
             return StdInput(False)
-        rd = items[0]
-        if len(rd) != 22 or rd[:2] != b"\x00\x14" or hash160(rd) != prev_script[2:22]:
-            return StdInput(False)
-        sig, pub = wit
-        ts = decode_tx_sig(sig, forkid)
-        if ts is None or not pubkey_bytes_ok(pub) or hash160(pub) != rd[2:22]:
-            return StdInput(False)
-        r, s, sh = ts
-        m = sighash_forkid(tx, p2pkh_script(rd[2:22]), value, i, sh, forkid)
-        return StdInput(True, m, r, s, pub)
+        rd, stack = items[-1], items[:-1]
+        wit = tx.witness[i] if i < len(tx.witness) else []
+        if len(rd) == 22 and rd[:2] == b"\x00\x14":
+            if stack or len(wit) != 2:
+                return StdInput(False)
+            sig, pub = wit
+            ts = decode_tx_sig(sig, forkid)
+            if ts is None or not pubkey_bytes_ok(pub) or hash160(pub) != rd[2:22]:
+                return StdInput(False)
+            r, s, sh = ts
+            m = sighash_forkid(tx, p2pkh_script(rd[2:22]), value, i, sh, forkid)
+            return StdInput(True, m, r, s, pub)
+        if len(rd) == 34 and rd[:2] == b"\x00\x20":
+            if stack:
+                return StdInput(False)
+            return _p2wsh_single(tx, i, rd[2:34], wit, value, forkid)
+        return _script_single(tx, i, rd, stack, value, forkid, False)
     return StdInput(False)
+
+
+def _p2pk_key(script: bytes) -> Optional[bytes]:
+    """The key of a direct-push P2PK script (21 <33> ac / 41 <65> ac)."""
+    if (len(script) == 35 and script[0] == 0x21 or len(script) == 67 and script[0] == 0x41) and script[-1] == 0xAC:
+        return script[1:-1]
+    return None
+
+
+def _script_single(tx: Tx, i: int, code: bytes, stack: List[bytes], value: int, forkid: Optional[int],
+                   segwit: bool) -> StdInput:
+    """A P2PK / P2PKH script (redeem or witness script) with its stack:
+    [sig] / [sig, pub]; sighash over `code`, legacy or BIP143."""
+    pub = _p2pk_key(code)
+    if pub is not None:
+        if len(stack) != 1 or not pubkey_bytes_ok(pub):
+            return StdInput(False)
+        sig = stack[0]
+    elif len(code) == 25 and code[:3] == b"\x76\xa9\x14" and code[23:] == b"\x88\xac":
+        if len(stack) != 2:
+            return StdInput(False)
+        sig, pub = stack
+        if not pubkey_bytes_ok(pub) or hash160(pub) != code[3:23]:
+            return StdInput(False)
+    else:
+        return StdInput(False)
+    ts = decode_tx_sig(sig, forkid)
+    if ts is None:
+        return StdInput(False)
+    r, s, sh = ts
+    m = sighash_forkid(tx, code, value, i, sh, forkid) if segwit else sighash_legacy(tx, code, value, i, sh, forkid)
+    return StdInput(True, m, r, s, pub)
+
+
+def _p2wsh_single(tx: Tx, i: int, prog: bytes, wit: List[bytes], value: int, forkid: Optional[int]) -> StdInput:
+    if not wit or hashlib.sha256(wit[-1]).digest() != prog:
+        return StdInput(False)
+    return _script_single(tx, i, wit[-1], list(wit[:-1]), value, forkid, True)
 
 
 def _record(msg32: bytes, r: int, s: int, pub: bytes) -> bytes:
@@ -731,13 +789,36 @@ class MultiSig:
 
 def std_multisig(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optional[int] = None
                  ) -> Optional[MultiSig]:
-    """Decode a bare or P2SH multisig input (None: not one, or it fails to
-    decode, i.e. verifyStdInput is False)."""
+    """Decode a bare, P2SH, P2WSH or P2SH-P2WSH multisig input (None: not
+    one, or it fails to decode, i.e. verifyStdInput is False). Segwit forms:
+    witness = [empty dummy] ++ items ++ [witness script], SHA-256(witness
+    script) == the program, empty scriptSig (nested: exactly the push of
+    00 20 <h32>), BIP143 sighash over the witness script; items follow the
+    scriptSig rules (empty = TxSignatureEmpty)."""
     if i >= len(tx.inputs):
         return None
+    ss = tx.inputs[i].script
+    wit = tx.witness[i] if i < len(tx.witness) else []
     p2sh = len(prev_script) == 23 and prev_script[:2] == b"\xa9\x14" and prev_script[22] == 0x87
-    if p2sh:
-        it = _multisig_items(tx.inputs[i].script, True)
+    prog = None
+    if len(prev_script) == 34 and prev_script[:2] == b"\x00\x20":
+        if ss:
+            return None
+        prog = prev_script[2:34]
+    elif p2sh:
+        pushes = _push_items(ss)
+        if pushes is not None and len(pushes) == 1 and len(pushes[0]) == 34 and pushes[0][:2] == b"\x00\x20":
+            if hash160(pushes[0]) != prev_script[2:22]:
+                return None
+            prog = pushes[0][2:34]
+    segwit = prog is not None
+    if segwit:
+        if len(wit) < 2 or wit[0] != b"" or hashlib.sha256(wit[-1]).digest() != prog:
+            return None
+        code = wit[-1]
+        items: List[Optional[bytes]] = [x if x else None for x in wit[1:-1]]
+    elif p2sh:
+        it = _multisig_items(ss, True)
         if it is None:
             return None
         items, code = it
@@ -745,7 +826,7 @@ def std_multisig(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optiona
             return None
     else:
         code = prev_script
-        it = _multisig_items(tx.inputs[i].script, False)
+        it = _multisig_items(ss, False)
         if it is None:
             return None
         items = it[0]
@@ -764,7 +845,12 @@ def std_multisig(tx: Tx, i: int, prev_script: bytes, value: int, forkid: Optiona
         sigs.append(ts)
     msgs = []
     for j in range(min(len(sigs), len(keys))):
-        msgs.append(ZERO32 if sigs[j] is None else sighash_legacy(tx, code, value, i, sigs[j][2], forkid))
+        if sigs[j] is None:
+            msgs.append(ZERO32)
+        elif segwit:
+            msgs.append(sighash_forkid(tx, code, value, i, sigs[j][2], forkid))
+        else:
+            msgs.append(sighash_legacy(tx, code, value, i, sigs[j][2], forkid))
     return MultiSig(m, keys, sigs, msgs)
 
 

@@ -347,8 +347,9 @@ def _device_verify_std(torch, ver, raw_txs, inputs, forkid):
 
 @pytest.mark.parametrize("forkid", [None, 0])
 def test_multisig_inputs_vs_oracle(torch, ver, coracle, forkid):
-    """Bare and P2SH m-of-n inputs (1-of-1 .. 15-of-15, 1-of-16; 22 valid and
-    adversarial variants, tests/txgen.py multisig_cases) shuffled into a
+    """Bare, P2SH, P2WSH and P2SH-P2WSH m-of-n inputs (1-of-1 .. 15-of-15,
+    1-of-16; up to 22 valid and adversarial variants, tests/txgen.py
+    multisig_cases) shuffled into a
     signed single-signature block: verdicts of the host and device entry
     points equal the oracle's countMulSig walk over C-oracle candidate
     verdicts, and the single-signature inputs are unaffected."""
@@ -370,7 +371,8 @@ def test_multisig_inputs_vs_oracle(torch, ver, coracle, forkid):
     assert not bad, bad[:10]
     assert _device_verify_std(torch, ver, raw, jobs, forkid) == got
     assert all(g for g, lb in zip(got, labels) if lb == "single")
-    assert sum(got) > len(bjobs) + 40
+    assert sum(got) > len(bjobs) + 80
+    assert {lb.split("-")[0] for lb in labels} == {"single", "bare", "p2sh", "p2wsh", "p2sh_p2wsh"}
 
 
 def test_multisig_many_inputs(torch, ver, coracle):
@@ -398,3 +400,27 @@ def test_multisig_many_inputs(torch, ver, coracle):
     got = hkv.verify_std_inputs(ver, txs, jobs)
     assert got == _ms_oracle(coracle, txs, jobs, None)
     assert got == [t % 3 != 0 for t in range(600)]
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_wrapped_single_sig_vs_oracle(torch, ver, coracle, forkid):
+    """P2SH-P2PK / P2SH-P2PKH / P2WSH-P2PK / P2WSH-P2PKH / P2SH-P2WSH-P2PK /
+    P2SH-P2WSH-P2PKH inputs, valid and mutated (tests/txgen.py
+    wrapped_single_cases): every 168-byte record byte-exact against the
+    oracle's std_input_record (sighash over the redeem / witness script, the
+    script-hash checks), verdicts equal to the oracle on the host and device
+    entry points."""
+    import hkv
+    rng = random.Random(299 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 3 != 0)) for k in range(8)]
+    txs, jobs, names = txgen.wrapped_single_cases(rng, keys, forkid)
+    raw = [sh.tx_serialize(t) for t in txs]
+    recs = device_std_records(torch, ver, raw, jobs, forkid)
+    exp = b"".join(sh.std_input_record(txs[t], i, p, v, forkid) for (t, i, p, v) in jobs)
+    bad = [names[k] for k in range(len(jobs)) if recs[k * 168:(k + 1) * 168] != exp[k * 168:(k + 1) * 168]]
+    assert not bad, bad[:10]
+    want = _ms_oracle(coracle, raw, jobs, forkid)
+    got = hkv.verify_std_inputs(ver, raw, jobs, forkid)
+    assert got == want, [(names[k], got[k], want[k]) for k in range(len(jobs)) if got[k] != want[k]][:10]
+    assert _device_verify_std(torch, ver, raw, jobs, forkid) == got
+    assert sum(got) >= 6 * 4 and len(got) - sum(got) >= 6 * 5

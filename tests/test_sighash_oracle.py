@@ -221,7 +221,8 @@ def test_multisig_oracle_labels(coracle, forkid):
     want = [nm.split("-", 2)[2] in MS_VALID for nm in names]
     bad = [(names[k], got[k]) for k in range(len(jobs)) if got[k] != want[k]]
     assert not bad, bad[:10]
-    assert sum(want) > 40 and len(want) - sum(want) > 200
+    assert sum(want) > 80 and len(want) - sum(want) > 400
+    assert {nm.split("-")[0] for nm in names} == {"bare", "p2sh", "p2wsh", "p2sh_p2wsh"}
 
 
 def test_multisig_candidate_order_and_walk():
@@ -238,3 +239,22 @@ def test_multisig_candidate_order_and_walk():
     ms1 = sh.MultiSig(1, [b"a", b"b"], [(1, 1, 1)], [sh.ZERO32])
     assert ms1.candidates() == [(0, 0), (0, 1)]
     assert ms1.resolve([False, True], [True, True])
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_wrapped_single_sig_oracle_labels(coracle, forkid):
+    """P2SH-P2PK / P2SH-P2PKH (legacy sighash over the redeem script) and
+    P2WSH-P2PK / P2WSH-P2PKH, native and P2SH-nested (BIP143 over the
+    witness script): valid spends verify; a corrupted signature, a wrong
+    script hash, an extra or missing stack item, a wrong key and high S fail;
+    NONE and ANYONECANPAY|SINGLE signatures made over their own sighash
+    verify."""
+    rng = random.Random(99 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 3 != 0)) for k in range(8)]
+    txs, jobs, names = txgen.wrapped_single_cases(rng, keys, forkid)
+    got = multisig_verdicts(coracle, txs, jobs, forkid)
+    # (a P2PK stack has no key: "wrong_pub" changes nothing there)
+    want = [nm.split("-")[1] in ("valid", "other_sighash", "acp_single")
+            or (nm.split("-")[1] == "wrong_pub" and nm.split("-")[0].endswith("_p2pk")) for nm in names]
+    bad = [(names[k], got[k]) for k in range(len(jobs)) if got[k] != want[k]]
+    assert not bad, bad[:10]

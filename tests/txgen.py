@@ -156,11 +156,15 @@ def _ms_tx(rng: random.Random) -> sh.Tx:
 OFF_CURVE = b"\x02" + (5).to_bytes(32, "big")   # x = 5: x^3 + 7 is not a square mod p
 
 
-def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = None):
-    """Bare and P2SH m-of-n inputs, valid and adversarial (one input per tx,
-    signatures made against the real scriptCode). Returns (txs, jobs, names)
-    with jobs = (tx index, input, prevout script, value); the verdict of each
-    is decided by the oracle (sighash_oracle.verify_std_input), not here."""
+def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = None,
+                   wraps=("bare", "p2sh", "p2wsh", "p2sh_p2wsh")):
+    """Bare, P2SH, P2WSH and P2SH-P2WSH m-of-n inputs, valid and adversarial
+    (one input per tx, signatures made against the real scriptCode: legacy
+    for bare / P2SH, BIP143 over the witness script for the segwit forms).
+    Returns (txs, jobs, names) with jobs = (tx index, input, prevout script,
+    value); the verdict of each is decided by the oracle
+    (sighash_oracle.verify_std_input), not here."""
+    import hashlib
     txs, jobs, names = [], [], []
     base_sh = 0x41 if forkid is not None else 0x01
     shapes = [(1, 1), (1, 2), (2, 2), (2, 3), (3, 5), (1, 3), (4, 7), (15, 15), (1, 16)]
@@ -169,17 +173,20 @@ def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = 
                 "bad_redeem_hash", "mixed_sighash", "bad_der_after_n", "trailing_op", "high_s", "all_empty",
                 "unknown_hashtype", "sig_past_end"]
     for (m, n) in shapes:
-        for p2sh in (False, True):
+        for wrap in wraps:
+            seg = wrap in ("p2wsh", "p2sh_p2wsh")
             for var in variants:
                 if var in ("swap",) and m < 2:
                     continue
                 if var in ("extra", "empty_skip_ok", "empty_skip_bad") and m == n:
                     continue
-                if p2sh is False and var == "bad_redeem_hash":
+                if wrap == "bare" and var == "bad_redeem_hash":
+                    continue
+                if seg and var in ("trailing_op", "sig_past_end"):
                     continue
                 ks = rng.sample(keys, n)
                 pubs = [k.pub for k in ks]
-                mm, nn = m, n
+                mm = m
                 if var == "off_curve_other":
                     pubs = pubs[:]
                     pubs[-1] = OFF_CURVE
@@ -194,13 +201,20 @@ def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = 
                 elif var == "pushdata1_key":
                     script = bytes([0x50 + m]) + b"\x4c" + bytes([len(pubs[0])]) + pubs[0] + \
                         b"".join(push(p) for p in pubs[1:]) + bytes([0x50 + n, 0xAE])
-                prev = p2sh_script(script) if p2sh else script
+                wprog = b"\x00\x20" + hashlib.sha256(script).digest()
+                if wrap == "bare":
+                    prev = script
+                elif wrap == "p2sh":
+                    prev = p2sh_script(script)
+                elif wrap == "p2wsh":
+                    prev = wprog
+                else:
+                    prev = p2sh_script(wprog)
                 if var == "bad_redeem_hash":
-                    prev = b"\xa9\x14" + bytes(20) + b"\x87"
+                    prev = b"\xa9\x14" + bytes(20) + b"\x87" if wrap != "p2wsh" else b"\x00\x20" + bytes(32)
                 tx = _ms_tx(rng)
                 i = rng.randrange(len(tx.inputs))
                 value = rng.randrange(1, 2**50)
-                # which keys sign, in key order
                 idx = sorted(rng.sample(range(n), m))
                 if var == "extra":
                     idx = sorted(rng.sample(range(n), m + 1))
@@ -218,7 +232,10 @@ def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = 
                     shs[0] = 0x04
                 items = []
                 for k, shb in zip(idx, shs):
-                    msg = sh.sighash_legacy(tx, script, value, i, shb, forkid)
+                    if seg:
+                        msg = sh.sighash_forkid(tx, script, value, i, shb, forkid)
+                    else:
+                        msg = sh.sighash_legacy(tx, script, value, i, shb, forkid)
                     d = ks[k].d
                     if var == "wrong_key" and k == idx[-1]:
                         d = rng.randrange(1, o.N)
@@ -228,23 +245,86 @@ def multisig_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = 
                     items.append(sh.der_encode(r, s) + bytes([shb]))
                 if var == "swap":
                     items[0], items[1] = items[1], items[0]
-                sig_part = b"".join(push(x) for x in items)
                 if var in ("empty_skip_ok", "empty_skip_bad"):
-                    sig_part = b"\x00" + sig_part
+                    items = [b""] + items
                 if var == "all_empty":
-                    sig_part = b"\x00" * m
+                    items = [b""] * m
                 if var == "bad_der_after_n":
-                    sig_part = sig_part + b"\x00" * (n - len(items)) + push(b"\x30\x02\x01\x01\x01")
-                if var == "sig_past_end":
-                    sig_part = sig_part + b"\x4c\x50\x30"
-                dummy = b"\x51" if var == "dummy_op1" else (b"" if var == "no_dummy" else b"\x00")
-                ss = dummy + sig_part
-                if var == "trailing_op":
-                    ss += b"\x75"   # OP_DROP: not a push, the decode fails
-                if p2sh:
-                    ss += push(script)
-                tx.inputs[i].script = ss
+                    items = items + [b""] * (n - len(items)) + [b"\x30\x02\x01\x01\x01"]
+                if seg:
+                    dummy = [b"\x01"] if var == "dummy_op1" else ([] if var == "no_dummy" else [b""])
+                    tx.witness[i] = dummy + items + [script]
+                    tx.inputs[i].script = push(wprog) if wrap == "p2sh_p2wsh" else b""
+                else:
+                    sig_part = b"".join(b"\x00" if not x else push(x) for x in items)
+                    if var == "sig_past_end":
+                        sig_part = sig_part + b"\x4c\x50\x30"
+                    dummy = b"\x51" if var == "dummy_op1" else (b"" if var == "no_dummy" else b"\x00")
+                    ss = dummy + sig_part
+                    if var == "trailing_op":
+                        ss += b"\x75"   # OP_DROP: not a push, the decode fails
+                    if wrap == "p2sh":
+                        ss += push(script)
+                    tx.inputs[i].script = ss
                 txs.append(tx)
                 jobs.append((len(txs) - 1, i, prev, value))
-                names.append(f"{'p2sh' if p2sh else 'bare'}-{m}of{n}-{var}")
+                names.append(f"{wrap}-{m}of{n}-{var}")
+    return txs, jobs, names
+
+
+def wrapped_single_cases(rng: random.Random, keys: List[Key], forkid: Optional[int] = None):
+    """Single-signature inputs behind P2SH / P2WSH (haskoin verifyStdInput's
+    ScriptHashInput and PayWitnessScriptHash branches): P2SH-P2PK,
+    P2SH-P2PKH, P2WSH-P2PK, P2WSH-P2PKH, P2SH-P2WSH-P2PK, P2SH-P2WSH-P2PKH,
+    valid and mutated. Returns (txs, jobs, names); verdicts by the oracle."""
+    import hashlib
+    txs, jobs, names = [], [], []
+    base_sh = 0x41 if forkid is not None else 0x01
+    kinds = ["p2sh_p2pk", "p2sh_p2pkh", "p2wsh_p2pk", "p2wsh_p2pkh", "p2sh_p2wsh_p2pk", "p2sh_p2wsh_p2pkh"]
+    variants = ["valid", "valid", "bad_sig", "bad_hash", "extra_item", "missing_item", "wrong_pub", "high_s",
+                "other_sighash", "acp_single"]
+    for kind in kinds:
+        for var in variants:
+            k = rng.choice(keys)
+            inner = push(k.pub) + b"\xac" if kind.endswith("_p2pk") else sh.p2pkh_script(k.h160)
+            seg = "p2wsh" in kind
+            wprog = b"\x00\x20" + hashlib.sha256(inner).digest()
+            if kind.startswith("p2sh_p2wsh"):
+                prev = p2sh_script(wprog)
+            elif kind.startswith("p2wsh"):
+                prev = wprog
+            else:
+                prev = p2sh_script(inner)
+            if var == "bad_hash":
+                prev = prev[:5] + bytes([prev[5] ^ 1]) + prev[6:]
+            tx = _ms_tx(rng)
+            i = rng.randrange(len(tx.inputs))
+            value = rng.randrange(1, 2**50)
+            shb = base_sh
+            if var == "other_sighash":
+                shb = 0x02 | (0x40 if forkid is not None else 0)
+            if var == "acp_single":
+                shb = 0x83 | (0x40 if forkid is not None else 0)
+            msg = sh.sighash_forkid(tx, inner, value, i, shb, forkid) if seg else \
+                sh.sighash_legacy(tx, inner, value, i, shb, forkid)
+            r, s = sign(msg, k.d, rng.randrange(1, o.N))
+            if var == "high_s":
+                s = o.N - s
+            sig = sh.der_encode(r, s) + bytes([shb])
+            if var == "bad_sig":
+                sig = sig[:6] + bytes([sig[6] ^ 4]) + sig[7:]
+            pub = k.pub if var != "wrong_pub" else Key(rng.randrange(1, o.N)).pub
+            stack = [sig] if kind.endswith("_p2pk") else [sig, pub]
+            if var == "extra_item":
+                stack = stack + [b"\x01"]
+            if var == "missing_item":
+                stack = stack[:-1]
+            if seg:
+                tx.witness[i] = stack + [inner]
+                tx.inputs[i].script = push(wprog) if kind.startswith("p2sh") else b""
+            else:
+                tx.inputs[i].script = b"".join(push(x) for x in stack) + push(inner)
+            txs.append(tx)
+            jobs.append((len(txs) - 1, i, prev, value))
+            names.append(f"{kind}-{var}")
     return txs, jobs, names
