@@ -185,9 +185,10 @@ verifyHashSigBatch c v xs =
     [(runPutS (serialize h), getCompactSig (exportCompactSig c s), exportPubKey c True p) | (h, s, p) <- xs]
 
 -- | Element i equals @verifyStdInput net ctx tx_i input_i so_i value_i@ for
--- P2PK / P2PKH / P2WPKH / P2SH-P2WPKH prevouts: template match, strict DER +
--- low S (decodeTxSig), HASH160, txSigHash / txSigHashForkId and
--- verifyHashSig all run on the GPU from the serialised txs.
+-- P2PK / P2PKH / P2WPKH / multisig prevouts, bare or behind P2SH / P2WSH /
+-- P2SH-P2WSH: template match, strict DER + low S (decodeTxSig), the HASH160
+-- / SHA-256 script checks, txSigHash / txSigHashForkId, verifyHashSig and
+-- the countMulSig walk all run on the GPU from the serialised txs.
 verifyStdInputBatch :: Verifier -> Network -> [Tx] -> [(Int, Int, ScriptOutput, Word64)] -> IO [Bool]
 verifyStdInputBatch v net txs ins = withMVar v.lock $ \_ -> do
   let raws = map (runPutS . serialize) txs
