@@ -190,22 +190,23 @@ HKV_DEV void shr_bits(uint32_t* a, int b) {
   for (int q = 0; q < L - 1; ++q) a[q] = (a[q] >> b) | (a[q + 1] << (32 - b));
   a[L - 1] >>= b;
 }
-// Radix-16 / radix-2^20 Booth recoding (LSB first, MSB-first consumption in
+// Radix-2^QW / radix-2^20 Booth recoding (LSB first, MSB-first consumption in
 // the ecmult kernel): d = ((v + 1) >> 1) - ((v >> W) << W), v = bits
-// [pos-1, pos+W-1]; sum_w d_w 16^w reproduces the scalar (< 2^131).
+// [pos-1, pos+W-1]; sum_w d_w 2^(QW w) reproduces the scalar (< 2^129).
 HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2,
                           uint32_t* SL, uint32_t* SH) {
+  constexpr uint32_t QM = (1u << QW) - 1u;
   uint32_t p1 = 0, p2 = 0;
 #pragma unroll 1
   for (int w = 0; w < NWIN; ++w) {
-    const uint32_t v1 = p1 | ((S1[0] & 15u) << 1), v2 = p2 | ((S2[0] & 15u) << 1);
-    p1 = (S1[0] >> 3) & 1u;
-    p2 = (S2[0] >> 3) & 1u;
-    shr_bits<5>(S1, 4);
-    shr_bits<5>(S2, 4);
-    const int d1 = (int)((v1 + 1u) >> 1) - (int)((v1 >> 4) << 4);
-    const int d2 = (int)((v2 + 1u) >> 1) - (int)((v2 >> 4) << 4);
-    im[(size_t)(IM_DIG + w) * n_pad + i] = (uint32_t)(d1 + 8) | ((uint32_t)(d2 + 8) << 5);
+    const uint32_t v1 = p1 | ((S1[0] & QM) << 1), v2 = p2 | ((S2[0] & QM) << 1);
+    p1 = (S1[0] >> (QW - 1)) & 1u;
+    p2 = (S2[0] >> (QW - 1)) & 1u;
+    shr_bits<5>(S1, QW);
+    shr_bits<5>(S2, QW);
+    const int d1 = (int)((v1 + 1u) >> 1) - (int)((v1 >> QW) << QW);
+    const int d2 = (int)((v2 + 1u) >> 1) - (int)((v2 >> QW) << QW);
+    im[(size_t)(IM_DIG + w) * n_pad + i] = (uint32_t)(d1 + QBIAS) | ((uint32_t)(d2 + QBIAS) << QDIG_BITS);
   }
   uint32_t pl = 0, ph = 0;
 #pragma unroll 1
@@ -459,7 +460,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       pj.y = p2.y;
       fe_set_u32(pj.z, 1);
 #pragma unroll 1
-      for (int j = 2; j < 8; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
+      for (int j = 2; j < QTAB_ENTRIES; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
         bool hz, rz;
         fe h;
         gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
@@ -474,12 +475,12 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       {
         fe bx;
         fe_mul(bx, pj.x, beta);
-        qtab_store(qs, n_lanes, lane, 7, 4, bx);
+        qtab_store(qs, n_lanes, lane, QTAB_ENTRIES - 1, 4, bx);
       }
       fe rho;
       fe_set_u32(rho, 1);
 #pragma unroll 1
-      for (int j = 6; j >= 0; --j) {
+      for (int j = QTAB_ENTRIES - 2; j >= 0; --j) {
         fe x, y, t;
         if (j >= 1) {
           qtab_load(qs, n_lanes, lane, j, 4, t);  // H_{j+1}
@@ -509,7 +510,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
     uint32_t dw = valid ? im[(size_t)(IM_DIG + NWIN - 1) * n_pad + i] : DIG_ZERO;
 #pragma unroll 1
     for (int win = NWIN - 1; win >= 0; --win) {
-      const int d1 = (int)(dw & 31u) - 8, d2 = (int)((dw >> 5) & 31u) - 8;
+      const int d1 = (int)(dw & QDIG_MASK) - QBIAS, d2 = (int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS;
       const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
       const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
@@ -530,7 +531,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
       }
       if (win != NWIN - 1) {
 #pragma unroll 1
-        for (int d = 0; d < 4; ++d) {
+        for (int d = 0; d < QW; ++d) {
           if (!inf) gej_double(acc, acc);
         }
       }

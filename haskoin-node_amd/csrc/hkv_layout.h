@@ -19,28 +19,42 @@ enum : int {
   IM_U1H = 31,    // 4 limbs, u1 bits 128..255
   IM_R = 35,      // 8 limbs, r (< n)
   IM_C = 43,      // 8 limbs, batch-inversion prefix product, then s^-1
-  IM_DIG = 51,    // 33 words: window w's radix-16 Booth digits of k1, k2
+  IM_DIG = 51,    // NWIN (<= 33) words: window w's radix-2^QW Booth digits of k1, k2
   IM_GDIG = 84,   // 2 x GWIN words: radix-2^GTAB_W Booth digits of u1_lo, u1_hi
   // between the parse and scalar kernels: s (normalised) and m = msg mod n
   IM_S = IM_K1,   // 8 limbs over K1|K2 (10 words)
   IM_M = IM_U1L,  // 8 limbs over U1L|U1H
 };
-// Q digit word of window w (w = 0..32, bit position 4w): biased Booth digits
-//   bits 0-4 d1 + 8 (k1, radix 16, -8..8), bits 5-9 d2 + 8 (k2)
+// Q digit word of window w (w = 0..NWIN-1, bit position QW*w): biased Booth
+//   digits, bits 0..QW d1 + QBIAS (k1, radix 2^QW, -QBIAS..QBIAS), bits
+//   QW+1..2QW+1 d2 + QBIAS (k2)
 // G digit word of G window j (j = 0..GWIN-1, bit position GTAB_W*j = Q
 // window GSTEP*j), one per u1 half: bits 0..GTAB_W-1 |d| (0..2^(GTAB_W-1)),
 // bit GTAB_W sign. Default radix 2^20: 7 windows, every fifth Q window.
+// HKV_QW = 5 (radix-32 Q windows: 52 instead of 66 Q additions, 125
+// doublings, a 16-entry table) is correct (GPU suite green) but measured
+// 1-1.5% slower at 1M (profiles/r02_variants.log): the 400 MB of per-lane
+// tables of a full grid no longer stay in the 256 MB MALL.
+#ifndef HKV_QW
+#define HKV_QW 4
+#endif
 #ifndef HKV_GTAB_W
 #define HKV_GTAB_W 20
 #endif
+constexpr int QW = HKV_QW;                       // Booth radix 2^QW of the k1 / k2 windows
+static_assert(QW == 4 || QW == 5, "radix-16 or radix-32 Q windows");
 constexpr int GTAB_W = HKV_GTAB_W;            // Booth radix of the fixed-base tables
-static_assert(GTAB_W % 4 == 0 && GTAB_W >= 8 && GTAB_W <= 28, "G windows sit on Q window boundaries");
-constexpr int NWIN = 33;
+static_assert(GTAB_W % QW == 0 && GTAB_W >= 8 && GTAB_W <= 28, "G windows sit on Q window boundaries");
+constexpr int NWIN = (130 + QW - 1) / QW;        // 33 / 26: |k| < 2^129 plus the Booth carry
+static_assert(IM_DIG + NWIN <= IM_GDIG, "digit words fit");
+constexpr int QBIAS = 1 << (QW - 1);             // digit range -QBIAS..QBIAS
+constexpr int QDIG_BITS = QW + 1;                // width of a biased digit in the digit word
+constexpr uint32_t QDIG_MASK = (1u << QDIG_BITS) - 1u;
 constexpr int GWIN = (128 + GTAB_W) / GTAB_W;  // covers 129 bits with the Booth carry
-constexpr int GSTEP = GTAB_W / 4;              // Q windows per G window
+constexpr int GSTEP = GTAB_W / QW;             // Q windows per G window
 constexpr uint32_t GD_MAG = (1u << GTAB_W) - 1u, GD_NEG = 1u << GTAB_W;
 constexpr int IM_WORDS = IM_GDIG + 2 * GWIN;
-constexpr uint32_t DIG_ZERO = 8u | (8u << 5);
+constexpr uint32_t DIG_ZERO = (uint32_t)QBIAS | ((uint32_t)QBIAS << QDIG_BITS);
 
 // signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
 // Montgomery's trick: 3(B-1) multiplications + 1 inversion)
@@ -54,10 +68,10 @@ constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF
 constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
 constexpr size_t GTAB_DWORDS = 2ull * GTAB_ENTRIES * 16;
 
-// Per-lane Q table: multiples j*Q, j = 1..8, affine on the lane's isomorphic
+// Per-lane Q table: multiples j*Q, j = 1..QBIAS, affine on the lane's isomorphic
 // curve; per entry 6 quads (16 B): x(2) | y(2) | beta*x(2); entry e of lane L
 // at quad (e * n_lanes + L) * 6 (hkv_kernels.hip qtab_ptr).
-constexpr int QTAB_ENTRIES = 8;
+constexpr int QTAB_ENTRIES = QBIAS;
 constexpr int QTAB_QUADS_PER_ENTRY = 6;
 constexpr int QTAB_QUADS = QTAB_ENTRIES * QTAB_QUADS_PER_ENTRY;
 

@@ -20,13 +20,15 @@ SC_RED = 8 * 4 + 5 * 4 + 4   # three folds by NC's low 128 bits
 SC_MUL = MUL256 + SC_RED
 SC_SQR = SQR256 + SC_RED
 
-GEJ_DOUBLE = 3 * FE_MUL + 4 * FE_SQR + FE_MUL_SMALL           # a=0, D = 4XB; 2^k scalings are shifts
+GEJ_DOUBLE = 3 * FE_MUL + 4 * FE_SQR + FE_MUL_SMALL           # a=0; the 1/2 scaling / 2^k are adds and shifts
 GEJ_ADD_GE = 8 * FE_MUL + 3 * FE_SQR                          # mixed add
 GEJ_ADD_ZINV = GEJ_ADD_GE + FE_MUL                            # + az = Z*Zg
 
-Q_WINDOWS = 33       # radix-16 Booth over 132 bits
+QW = 4               # Booth radix 2^QW of the k1 / k2 windows (hkv_layout.h HKV_QW)
+Q_WINDOWS = (130 + QW - 1) // QW     # 26 (radix 32) / 33 (radix 16)
+Q_TABLE = 1 << (QW - 1)              # j*Q, j = 1..16 (radix 32) / 1..8
 G_WINDOWS = 7        # radix-2^20 Booth over 140 bits (u1 halves)
-DOUBLINGS = 4 * (Q_WINDOWS - 1)
+DOUBLINGS = QW * (Q_WINDOWS - 1)
 
 SC_INV_LOW = 0x0BAAEDCE6AF48A03BBFD25E8CD036413F
 BATCH_INV = 16       # signatures per s^-1 (hkv_layout.h)
@@ -35,10 +37,10 @@ BATCH_INV = 16       # signatures per s^-1 (hkv_layout.h)
 def ecmult_products() -> int:
     table = (GEJ_DOUBLE                      # 2Q
              + FE_SQR + 3 * FE_MUL           # Q' = (x Z^2, y Z^3)
-             + 6 * GEJ_ADD_GE                # 3Q .. 8Q
+             + (Q_TABLE - 2) * GEJ_ADD_GE    # 3Q .. Q_TABLE*Q
              + FE_MUL                        # Zg
-             + FE_MUL                        # beta * x of entry 8
-             + 6 * (5 * FE_MUL + FE_SQR)     # rescale entries 2..7 (+ rho step, beta)
+             + FE_MUL                        # beta * x of the last entry
+             + (Q_TABLE - 2) * (5 * FE_MUL + FE_SQR)   # rescale entries 2..Q_TABLE-1 (+ rho step, beta)
              + (4 * FE_MUL + FE_SQR))        # rescale entry 1
     ladder = DOUBLINGS * GEJ_DOUBLE + 2 * Q_WINDOWS * GEJ_ADD_GE + 2 * G_WINDOWS * GEJ_ADD_ZINV
     compare = 3 * FE_MUL + FE_SQR

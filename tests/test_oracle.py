@@ -60,14 +60,19 @@ def booth(k, w, nwin):
 
 
 def test_booth_recoding_identity():
-    """Radix-16 (Q) / radix-2^20 (G, hkv_layout.h GTAB_W) Booth digits as the
-    ecmult kernel extracts them."""
+    """Radix-32 (Q, hkv_layout.h HKV_QW = 5; radix 16 for HKV_QW = 4) /
+    radix-2^20 (G, GTAB_W) Booth digits as the ecmult kernel extracts them:
+    26 radix-32 windows carry any |k| < 2^129 the GLV split produces."""
     rng = random.Random(9)
     for _ in range(2000):
         k = rng.randrange(2**131)
         d = booth(k, 4, 33)
         assert all(-8 <= x <= 8 for x in d)
         assert sum(x * 16**i for i, x in enumerate(d)) == k
+        k = rng.choice([rng.randrange(2**129), 2**129 - 1 - rng.randrange(2**20)])
+        d = booth(k, 5, 26)
+        assert all(-16 <= x <= 16 for x in d)
+        assert sum(x * 32**i for i, x in enumerate(d)) == k
         u = rng.randrange(2**128)
         e = booth(u, 20, 7)                        # GWIN = 7 windows of 20 bits
         assert all(-2**19 <= x <= 2**19 for x in e)
