@@ -392,6 +392,37 @@ HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32
   a.v[4] = v1.x; a.v[5] = v1.y; a.v[6] = v1.z; a.v[7] = v1.w;
 }
 
+// SPLIT mode keeps each lane's half of the Q table in LDS: entry j holds
+// (x, y) for k1 * Q (half 0) or (beta*x, y) for k2 * lambda(Q) (half 1), as
+// four uint4 quads at [j][quad][thread] (a wave's 64 lanes read 1 KB
+// contiguous per quad). 8 entries x 64 B x 256 threads = 128 KB; with
+// < 1 wave per SIMD the LDS latency replaces an L2 round trip per lookup.
+// HKV_SPLIT_QLDS=0 keeps the table in scratch as the full-grid kernel does.
+// SPLIT launches run < 1 wave per SIMD, so they take the whole register
+// file (196 VGPRs, no spill) instead of the full grid's 4-wave budget.
+#ifndef HKV_SPLIT_WAVES
+#define HKV_SPLIT_WAVES 1
+#endif
+#ifndef HKV_SPLIT_QLDS
+#define HKV_SPLIT_QLDS 1
+#endif
+constexpr int QLDS_ENTRIES = (HKV_SPLIT_QLDS && QTAB_ENTRIES <= 8) ? QTAB_ENTRIES : 0;
+HKV_DEV void qlds_store(uint4* t, int entry, const fe& x, const fe& y) {
+  uint4* p = t + (size_t)entry * 4 * WG + threadIdx.x;
+  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  p[WG] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  p[2 * WG] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+  p[3 * WG] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+}
+HKV_DEV void qlds_load(const uint4* t, int entry, fe& x, fe& y) {
+  const uint4* p = t + (size_t)entry * 4 * WG + threadIdx.x;
+  const uint4 v0 = p[0], v1 = p[WG], v2 = p[2 * WG], v3 = p[3 * WG];
+  x.v[0] = v0.x; x.v[1] = v0.y; x.v[2] = v0.z; x.v[3] = v0.w;
+  x.v[4] = v1.x; x.v[5] = v1.y; x.v[6] = v1.z; x.v[7] = v1.w;
+  y.v[0] = v2.x; y.v[1] = v2.y; y.v[2] = v2.z; y.v[3] = v2.w;
+  y.v[4] = v3.x; y.v[5] = v3.y; y.v[6] = v3.z; y.v[7] = v3.w;
+}
+
 // SPLIT (small batches, when one lane per signature would leave the GPU
 // half empty): a workgroup takes 128 signatures; waves 0-1 run the k1*Q and
 // u1_lo*G half of the sum, waves 2-3 the k2*(lambda Q) and u1_hi*(2^128 G)
@@ -401,14 +432,18 @@ HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32
 // dependency chain shrinks by about a quarter; total work grows by the
 // duplicated doublings and table, so large batches use SPLIT = false.
 template <bool SPLIT>
-__global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
+__global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits,
                                                         unsigned long long* __restrict__ clk) {
-  // per wave: two G-entry slots, each 4 quads x 64 lanes x 16 B (LDS-DMA target);
-  // in SPLIT mode reused after the window loop for the half-sum exchange
-  __shared__ __attribute__((aligned(16))) uint4 gpf[WG / 64][2][4][64];
+  // per wave: two G-entry slots (one in SPLIT mode: a wave adds one G term),
+  // each 4 quads x 64 lanes x 16 B (LDS-DMA target); in SPLIT mode reused
+  // after the window loop for the half-sum exchange
+  constexpr int GSLOTS = SPLIT ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) uint4 gpf[WG / 64][GSLOTS][4][64];
+  constexpr bool QLDS = SPLIT && QLDS_ENTRIES > 0;
+  __shared__ __attribute__((aligned(16))) uint4 qlds[QLDS ? QLDS_ENTRIES * 4 * WG : 1];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ln = threadIdx.x & 63;
   constexpr uint32_t PER_WG = SPLIT ? WG / 2 : WG;
@@ -476,6 +511,7 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         fe bx;
         fe_mul(bx, pj.x, beta);
         qtab_store(qs, n_lanes, lane, QTAB_ENTRIES - 1, 4, bx);
+        if (QLDS) qlds_store(qlds, QTAB_ENTRIES - 1, half ? bx : pj.x, pj.y);
       }
       fe rho;
       fe_set_u32(rho, 1);
@@ -492,6 +528,11 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         fe_mul(x, x, t);
         fe_mul(t, t, rho);
         fe_mul(y, y, t);
+        if (QLDS) {
+          if (half) fe_mul(x, x, beta);
+          qlds_store(qlds, j, x, y);
+          continue;
+        }
         qtab_store(qs, n_lanes, lane, j, 0, x);
         qtab_store(qs, n_lanes, lane, j, 2, y);
         fe_mul(x, x, beta);
@@ -525,8 +566,12 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         const uint4* e1 = reinterpret_cast<const uint4*>(gtab) + ((size_t)GTAB_ENTRIES + (m1 ? m1 - 1 : 0)) * 4;
 #pragma unroll
         for (int qd = 0; qd < 4; ++qd) {
-          __builtin_amdgcn_global_load_lds(e0 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][0][qd][0], 16, 0, 0);
-          __builtin_amdgcn_global_load_lds(e1 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][1][qd][0], 16, 0, 0);
+          if (SPLIT) {  // one G term per wave
+            __builtin_amdgcn_global_load_lds((half ? e1 : e0) + qd, (__attribute__((address_space(3))) void*)&gpf[wv][0][qd][0], 16, 0, 0);
+          } else {
+            __builtin_amdgcn_global_load_lds(e0 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][0][qd][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(e1 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][GSLOTS - 1][qd][0], 16, 0, 0);
+          }
         }
       }
       if (win != NWIN - 1) {
@@ -543,8 +588,12 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
         const bool take = dg != 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
         fe tx, ty;
-        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
-        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
+        if (QLDS) {
+          qlds_load(qlds, (slot == 0 ? i1 : i2), tx, ty);
+        } else {
+          qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
+          qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
+        }
         fe nty;
         fe_neg(nty, ty);
         fe_cmov(ty, nty, neg);
@@ -564,8 +613,9 @@ __global__ void __launch_bounds__(WG, HKV_ECMULT_WAVES) hkv_ecmult_kernel(const 
           const bool take = (gd & GD_MAG) != 0;
           fe tx, ty;
           {
-            const uint4 a0 = gpf[wv][slot][0][ln], a1 = gpf[wv][slot][1][ln];
-            const uint4 a2 = gpf[wv][slot][2][ln], a3 = gpf[wv][slot][3][ln];
+            const int gs = SPLIT ? 0 : slot;
+            const uint4 a0 = gpf[wv][gs][0][ln], a1 = gpf[wv][gs][1][ln];
+            const uint4 a2 = gpf[wv][gs][2][ln], a3 = gpf[wv][gs][3][ln];
             tx.v[0] = a0.x; tx.v[1] = a0.y; tx.v[2] = a0.z; tx.v[3] = a0.w;
             tx.v[4] = a1.x; tx.v[5] = a1.y; tx.v[6] = a1.z; tx.v[7] = a1.w;
             ty.v[0] = a2.x; ty.v[1] = a2.y; ty.v[2] = a2.z; ty.v[3] = a2.w;
