@@ -4,7 +4,8 @@
 //   1. hkv_prologue_kernel  — record parse (compact sig + SEC1 pubkey incl.
 //      hybrid keys and sqrt decompression), high-S policy, m = msg mod n,
 //      s^-1, u1 = m/s, u2 = r/s, GLV split of u2. Writes a SoA intermediate.
-//   2. hkv_ecmult_kernel    — per-lane table of 1..8 * Q on an isomorphic
+//   2. hkv_ecmult_kernel    — per-lane table of 1..2^(QW-1) * Q (8 entries at the
+//      default radix 16) on an isomorphic
 //      curve (one common Z, so all Q additions are mixed), then a shared
 //      doubling chain of 132 bits with radix-16 Booth digits for k1*Q and
 //      k2*(lambda Q) and radix-2^20 Booth digits for u1_lo*G and
@@ -473,10 +474,11 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
     if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
     const bool neg1 = (flags & FLAG_NEG1) != 0, neg2 = (flags & FLAG_NEG2) != 0;
 
-    // ---- table: j*Q, j = 1..8, on the isomorphic curve of scale Zg ----
+    // ---- table: j*Q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
     // Pass 1 streams raw entries to the lane's scratch (z-ratios H_j parked in
     // the beta*x slot of entry j-1); pass 2 walks back rescaling every entry
-    // to the common Z (rho_j = prod_{k>j} H_k) and writes beta*x.
+    // to the common Z (rho_j = prod_{k>j} H_k) and writes beta*x (SPLIT mode:
+    // the rescaled entries of the wave's half go to LDS instead).
     fe Zg;
     {
       gej p2, pj;
