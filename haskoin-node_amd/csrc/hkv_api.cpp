@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hkv.h"
@@ -53,8 +54,10 @@ struct DevCtx {
   // [6] host-form verdict words
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t* ms_total = nullptr;  // pinned: off[n] (candidates | keys << 32)
-  hipEvent_t ms_ev = nullptr;
+  uint64_t* ms_total = nullptr;  // pinned: [0] sum (candidates | keys << 32), [1] sequence number
+  uint64_t ms_seq = 0;           // last sequence number handed to hkv_ms_scan_kernel
+  uint64_t* ms_total_dev = nullptr;  // its device-side address
+  void* ms_ctr = nullptr;            // device counters of hkv_ms_scan_kernel
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -123,8 +126,10 @@ int scratch_release(DevCtx& d, hipStream_t st) {
   return HKV_OK;
 }
 
-// enqueue prologue + ecmult for n records at d_records; verdict words in d.bits
-int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st) {
+// enqueue prologue + ecmult for n records at d_records; verdict words in
+// out_bits ((n + 31) / 32 words, device memory) or, when null, in d.bits
+int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st,
+                   uint32_t* out_bits = nullptr) {
   const size_t n_pad = round_up(n, hkv::WG);
   int rc = ensure_dev_buffers(d, n_pad);
   if (rc) return rc;
@@ -151,8 +156,9 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
-  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, d.bits, split,
-                             d.profile ? d.clk : nullptr, st),
+  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, out_bits ? out_bits : d.bits,
+                             (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32), split, d.profile ? d.clk : nullptr,
+                             st),
           "ecmult launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
@@ -175,8 +181,16 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
   HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
   HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
-  HKV_TRY(hipEventCreateWithFlags(&d.ms_ev, hipEventDisableTiming), "hipEventCreate(multisig)");
-  HKV_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.ms_total), sizeof(uint64_t)), "hipHostMalloc(multisig)");
+  // fine-grained and mapped: hkv_ms_scan_kernel stores the multisig sum here
+  HKV_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.ms_total), 2 * sizeof(uint64_t),
+                        hipHostMallocCoherent | hipHostMallocMapped),
+          "hipHostMalloc(multisig)");
+  HKV_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d.ms_total_dev), d.ms_total, 0),
+          "hipHostGetDevicePointer(multisig)");
+  // total + finished-workgroup count; the scan kernel re-arms them itself
+  HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
+  HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
+  HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
   HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
   HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 64 MiB at radix 2^20
@@ -214,7 +228,7 @@ void free_device(DevCtx& d) {
   for (auto p : d.ms)
     if (p) (void)hipFree(p);
   if (d.ms_total) (void)hipHostFree(d.ms_total);
-  if (d.ms_ev) (void)hipEventDestroy(d.ms_ev);
+  if (d.ms_ctr) (void)hipFree(d.ms_ctr);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.clk) (void)hipFree(d.clk);
   if (d.last_use) (void)hipEventDestroy(d.last_use);
@@ -309,21 +323,39 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   int rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   if (rc) return rc;
   rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
-  if (!rc) rc = grow(&d.ms[1], &d.ms_cap[1], 8, "hipMalloc(multisig total)");
   if (!rc) rc = grow(&d.ms[2], &d.ms_cap[2], n * 8, "hipMalloc(multisig offsets)");
   if (rc) return rc;
   uint32_t* desc = static_cast<uint32_t*>(d.ms[0]);
   uint64_t* off = static_cast<uint64_t*>(d.ms[2]);
+  // The scan kernel's last workgroup stores the sum, then the sequence
+  // number, into the pinned words; the host polls them while the main
+  // verify runs (an event record here would put a barrier packet between
+  // the scan and the verify, ~5 us on the block path).
+  volatile uint64_t* hv = d.ms_total;
+  const uint64_t seq = ++d.ms_seq;
+  if (n == 0) {  // no launch: publish the empty sum here
+    hv[0] = 0;
+    hv[1] = seq;
+  }
   HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
-                              desc, off, static_cast<uint64_t*>(d.ms[1]), st),
+                              desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq, st),
           "multisig scan launch");
-  HKV_TRY(hipMemcpyAsync(d.ms_total, d.ms[1], sizeof(uint64_t), hipMemcpyDeviceToHost, st), "D2H multisig total");
-  HKV_TRY(hipEventRecord(d.ms_ev, st), "hipEventRecord(multisig)");
-  rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st);
+  rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
   if (rc) return rc;
-  HKV_TRY(hipMemcpyAsync(out_bits, d.bits, (n + 31) / 32 * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
-  HKV_TRY(hipEventSynchronize(d.ms_ev), "multisig total sync");
-  const uint64_t total = *d.ms_total;
+  for (uint32_t spin = 1; hv[1] != seq; ++spin) {
+    if ((spin & 255u) == 0) {  // a failed launch never publishes: fall back to the stream's state
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipErrorNotReady) {
+        std::this_thread::yield();
+        continue;
+      }
+      if (hv[1] == seq) break;
+      if (q != hipSuccess) return hip_fail(q, "multisig scan");
+      g_last_hip = "multisig scan finished without publishing its sum";
+      return HKV_E_INTERNAL;
+    }
+  }
+  const uint64_t total = hv[0];
   const size_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
   if (n_keys == 0) return HKV_OK;  // no multisig input
   rc = grow(&d.ms[4], &d.ms_cap[4], (n_cand + n_keys) * hkv::REC_SIZE, "hipMalloc(multisig records)");
@@ -583,10 +615,8 @@ int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, ui
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = scratch_acquire(d, st);
-  if (!rc) rc = enqueue_verify(d, d_records, n, mode, st);
+  if (!rc) rc = enqueue_verify(d, d_records, n, mode, st, d_bits);
   if (rc) return rc;
-  const size_t words = (n + 31) / 32;
-  HKV_TRY(hipMemcpyAsync(d_bits, d.bits, words * 4, hipMemcpyDeviceToDevice, st), "bits D2D");
   return scratch_release(d, st);
 }
 

@@ -28,7 +28,8 @@ namespace hkv {
 hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im, bool split,
                            hipStream_t st);
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, bool split, unsigned long long* clk, hipStream_t st);
+                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, unsigned long long* clk,
+                         hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
 hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,
@@ -51,7 +52,8 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
 // multisig inputs (hkv_sighash.hip section 4; pubkey check in hkv_kernels.hip)
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
-                          uint32_t* desc, uint64_t* off, uint64_t* total, hipStream_t st);
+                          uint32_t* desc, uint64_t* off, uint64_t* counters, uint64_t* host_total, uint64_t seq,
+                          hipStream_t st);
 hipError_t launch_ms_emit(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                           const uint32_t* desc, const uint64_t* off, uint8_t* cand, uint8_t* keyrec, hipStream_t st);

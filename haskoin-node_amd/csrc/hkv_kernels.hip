@@ -436,7 +436,7 @@ template <bool SPLIT>
 __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
-                                                        uint32_t* __restrict__ bits,
+                                                        uint32_t* __restrict__ bits, uint32_t n_words,
                                                         unsigned long long* __restrict__ clk) {
   // per wave: two G-entry slots (one in SPLIT mode: a wave adds one G term),
   // each 4 quads x 64 lanes x 16 B (LDS-DMA target); in SPLIT mode reused
@@ -716,11 +716,11 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
     }
     const uint64_t ball = __ballot(accept);
     if ((threadIdx.x & 63) == 0 && half == 0) {
-      const uint32_t wbase = base + (sub & ~63u);
-      if (wbase < n_pad) {
-        bits[wbase / 32] = (uint32_t)ball;
-        bits[wbase / 32 + 1] = (uint32_t)(ball >> 32);
-      }
+      // n_words bounds the caller's bitmap ((n + 31) / 32 words when the
+      // verdicts go straight to the API's output, n_pad / 32 for d.bits)
+      const uint32_t wi = (base + (sub & ~63u)) / 32;
+      if (wi < n_words) bits[wi] = (uint32_t)ball;
+      if (wi + 1 < n_words) bits[wi + 1] = (uint32_t)(ball >> 32);
     }
   }
   if (clk != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1045,11 +1045,14 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   return hipGetLastError();
 }
 hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, bool split, unsigned long long* clk, hipStream_t st) {
+                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, unsigned long long* clk,
+                         hipStream_t st) {
   if (split)
-    hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, clk);
+    hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, n_words,
+                       clk);
   else
-    hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, clk);
+    hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, n_words,
+                       clk);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {

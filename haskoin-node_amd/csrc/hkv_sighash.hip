@@ -538,14 +538,11 @@ HKV_DEV uint32_t walk_witness(const uint8_t* T, uint32_t wstart, uint32_t i) {
 // ---------------------------------------------------------------------------
 // 1. tx index
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restrict__ txs,
-                                                          const uint32_t* __restrict__ tx_off, uint32_t n_tx,
-                                                          uint32_t want_bip143, uint32_t* __restrict__ txt) {
-  const uint32_t t = blockIdx.x * WG + threadIdx.x;
-  const bool live = t < n_tx;
-  uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+// bounds-checked parse of tx t's wire form into the first 8 words of its row
+HKV_DEV void tx_index_row(const uint8_t* __restrict__ txs, const uint32_t* __restrict__ tx_off, uint32_t t,
+                          uint32_t row[8]) {
   bool ok = false;
-  if (live) {
+  {
     const uint32_t st = tx_off[t], end = tx_off[t + 1];
     ok = end >= st && end - st >= 10;
     uint32_t off = st + 4, nin = 0, nout = 0;
@@ -591,22 +588,40 @@ __global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restr
     row[TXT_OUTS_END] = outs_end;
     row[TXT_LOCK] = off;
     row[TXT_START] = st;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + k] = row[k];
   }
-  (void)want_bip143;  // the BIP143 hashes: hkv_tx_hash_kernel
+}
+
+__global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restrict__ txs,
+                                                          const uint32_t* __restrict__ tx_off, uint32_t n_tx,
+                                                          uint32_t* __restrict__ txt) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= n_tx) return;
+  uint32_t row[8];
+  tx_index_row(txs, tx_off, t, row);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + k] = row[k];
 }
 
 // 1b. the three BIP143 per-tx hashes, one lane per (tx, hash): blockIdx.y
 // selects hashPrevouts / hashSequence / hashOutputs (wave-uniform), so the
 // three SHA-256d streams of a tx run side by side instead of one after the
 // other (a block's index is latency-bound: one wave per 64 txs).
-__global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
+// Each lane parses its tx itself (the three blockIdx.y lanes of a tx repeat
+// the cheap walk; y = 0 writes the row), so the index costs no launch of its own.
+__global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restrict__ txs,
+                                                         const uint32_t* __restrict__ tx_off, uint32_t n_tx,
                                                          uint32_t* __restrict__ txt) {
   __shared__ uint32_t buf[16 * WG];
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
   const uint32_t which = blockIdx.y;  // 0 prevouts, 1 sequences, 2 outputs
-  const uint32_t* row = txt + (size_t)(t < n_tx ? t : 0) * TXT_WORDS;
+  uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (t < n_tx) {
+    tx_index_row(txs, tx_off, t, row);
+    if (which == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + k] = row[k];
+    }
+  }
   const bool go = t < n_tx && (row[TXT_FLAGS] & TXF_OK);
   Gen g;
   uint32_t h[8], d[8];
@@ -1323,7 +1338,11 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
                                                          const hkv_input_job* __restrict__ jobs, uint32_t n,
                                                          int32_t forkid, uint32_t* __restrict__ desc,
                                                          uint64_t* __restrict__ off,
-                                                         unsigned long long* __restrict__ total) {
+                                                         unsigned long long* __restrict__ counters,
+                                                         volatile unsigned long long* __restrict__ host_total,
+                                                         unsigned long long seq) {
+  unsigned long long* total = counters;                                  // candidates | keys << 32
+  unsigned int* done = reinterpret_cast<unsigned int*>(counters + 1);    // finished workgroups
   __shared__ uint32_t buf[16 * WG];
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   MsIn r;
@@ -1374,6 +1393,20 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
     // record ranges: candidates in the low 32 bits, key checks in the high 32
     // (their sums stay below 2^32); placement order is irrelevant to verdicts
     off[jx] = ok ? (uint64_t)atomicAdd(total, (unsigned long long)r.n_cand | ((unsigned long long)r.n << 32)) : 0ull;
+  }
+  // The last workgroup to finish publishes the sum to the caller's pinned
+  // host word and re-arms both device counters, so the stream carries no
+  // memset and no D2H copy (the host waits on an event after this kernel).
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
+    __threadfence();
+    const unsigned long long t = atomicExch(total, 0ull);
+    atomicExch(done, 0u);
+    host_total[0] = t;
+    __threadfence_system();
+    host_total[1] = seq;  // the host polls this word
+    __threadfence_system();
   }
 }
 
@@ -1532,11 +1565,10 @@ static inline uint32_t blocks_for(size_t n) { return (uint32_t)((n + WG - 1) / W
 hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t want_bip143,
                            uint32_t* txt, hipStream_t st) {
   if (n_tx == 0) return hipSuccess;
-  hipLaunchKernelGGL(hkv_tx_index_kernel, dim3(blocks_for(n_tx)), dim3(WG), 0, st, txs, tx_off, n_tx, want_bip143,
-                     txt);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !want_bip143) return e;
-  hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3(blocks_for(n_tx), 3), dim3(WG), 0, st, txs, n_tx, txt);
+  if (want_bip143)
+    hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3(blocks_for(n_tx), 3), dim3(WG), 0, st, txs, tx_off, n_tx, txt);
+  else
+    hipLaunchKernelGGL(hkv_tx_index_kernel, dim3(blocks_for(n_tx)), dim3(WG), 0, st, txs, tx_off, n_tx, txt);
   return hipGetLastError();
 }
 hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
@@ -1567,11 +1599,12 @@ namespace hkv {
 // number of candidate records | key-check records << 32
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
-                          uint32_t* desc, uint64_t* off, uint64_t* total, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(total, 0, sizeof(uint64_t), st);
-  if (e != hipSuccess) return e;
+                          uint32_t* desc, uint64_t* off, uint64_t* counters, uint64_t* host_total, uint64_t seq,
+                          hipStream_t st) {
+  if (n == 0) return hipSuccess;  // the caller publishes the empty sum itself
   hipLaunchKernelGGL(hkv_ms_scan_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts, scripts_len,
-                     jobs, n, forkid, desc, off, reinterpret_cast<unsigned long long*>(total));
+                     jobs, n, forkid, desc, off, reinterpret_cast<unsigned long long*>(counters),
+                     reinterpret_cast<volatile unsigned long long*>(host_total), (unsigned long long)seq);
   return hipGetLastError();
 }
 hipError_t launch_ms_emit(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
