@@ -163,6 +163,59 @@ HKV_DEV void gej_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, con
     inf = inf || (degen && !rz);             // T == -acc
   }
 }
+// ---- paired-product forms for a lone wave per SIMD ----
+// Same results as gej_double / gej_accumulate; independent field products
+// are issued as interleaved pairs (fe_mul2 / fe_sqr2 / fe_sqrmul), so the
+// dependency stalls of one product are filled by the other. The small-batch
+// split kernel runs < 1 wave per SIMD, where a single product's chain leaves
+// a third of the issue slots empty (tools/ubench_field.hip, blocks_per_cu 1).
+HKV_DEV void gej_double_ilp(gej& r, const gej& a) {
+  fe A, B, M, Z3, C, E, t;
+  fe_sqr2(A, a.x, B, a.y);
+  fe_mul2(M, a.x, B, Z3, a.y, a.z);  // M = XB, Z3' = YZ
+  fe_mul_small(E, A, 3);
+  fe_half(E, E);                     // E' = 3A/2
+  fe_sqr2(C, B, t, E);               // C = B^2, E'^2
+  r.z = Z3;
+  fe_shl(B, M, 1);
+  fe_sub(r.x, t, B);                 // X3' = E'^2 - 2M
+  fe_sub(t, M, r.x);
+  fe_mul(t, E, t);
+  fe_sub(r.y, t, C);                 // Y3' = E'(M - X3') - C
+}
+
+HKV_DEV void gej_accumulate_ilp(gej& acc, bool& inf, const fe& az, const fe& tx, const fe& ty, bool take) {
+  fe h, rr, hh;
+  {
+    fe z2, t;
+    fe_sqr(z2, az);
+    fe_mul2(h, tx, z2, t, az, z2);    // U2, az^3
+    fe_sub(h, h, acc.x);              // H = U2 - X1
+    fe_sqrmul(hh, h, rr, ty, t);      // H^2, S2
+  }
+  fe_sub(rr, rr, acc.y);              // R = S2 - Y1
+  const bool live = take && !inf;
+  const bool hz = fe_is_zero(h);
+  if (live && !hz) {
+    fe hhh, v, r2, z3, t2;
+    fe_mul2(hhh, h, hh, v, acc.x, hh);  // H^3, V = X1 H^2
+    fe_sqrmul(r2, rr, z3, acc.z, h);    // R^2, Z3 = Z1 H
+    acc.z = z3;
+    fe_sub(r2, r2, hhh);
+    fe_shl(t2, v, 1);
+    fe_sub(acc.x, r2, t2);              // X3 = R^2 - H^3 - 2V
+    fe_sub(v, v, acc.x);
+    fe_mul2(v, rr, v, hhh, acc.y, hhh);
+    fe_sub(acc.y, v, hhh);              // Y3 = R(V - X3) - Y1 H^3
+  }
+  const bool degen = live && hz;
+  if (__builtin_expect(__any(degen), 0)) {
+    const bool rz = fe_is_zero(rr);
+    if (degen && rz) gej_double(acc, acc);   // T == acc
+    inf = inf || (degen && !rz);             // T == -acc
+  }
+}
+
 // acc := (itx, ity, 1) on lanes that take a point while at infinity
 HKV_DEV void gej_accumulate_from_inf(gej& acc, bool& inf, const fe& itx, const fe& ity, bool take) {
   const bool f = take && inf;

@@ -432,6 +432,23 @@ HKV_DEV void qlds_load(const uint4* t, int entry, fe& x, fe& y) {
 // LDS for one Jacobian addition before the x compare. The per-signature
 // dependency chain shrinks by about a quarter; total work grows by the
 // duplicated doublings and table, so large batches use SPLIT = false.
+// SPLIT launches use the paired-product group forms (HKV_SPLIT_ILP=0: the
+// plain ones); the full grid keeps the plain forms, its 4 waves per SIMD
+// already fill the issue slots.
+#ifndef HKV_SPLIT_ILP
+#define HKV_SPLIT_ILP 1
+#endif
+template <bool ILP>
+HKV_DEV void ec_double(gej& acc) {
+  if constexpr (ILP) gej_double_ilp(acc, acc);
+  else gej_double(acc, acc);
+}
+template <bool ILP>
+HKV_DEV void ec_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, const fe& ty, bool take) {
+  if constexpr (ILP) gej_accumulate_ilp(acc, inf, az, tx, ty, take);
+  else gej_accumulate(acc, inf, az, tx, ty, take);
+}
+
 template <bool SPLIT>
 __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
@@ -579,7 +596,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
       if (win != NWIN - 1) {
 #pragma unroll 1
         for (int d = 0; d < QW; ++d) {
-          if (!inf) gej_double(acc, acc);
+          if (!inf) ec_double<SPLIT && HKV_SPLIT_ILP>(acc);
         }
       }
       // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
@@ -600,7 +617,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
         fe_neg(nty, ty);
         fe_cmov(ty, nty, neg);
         const bool was_inf = inf;
-        gej_accumulate(acc, inf, acc.z, tx, ty, take);
+        ec_accumulate<SPLIT && HKV_SPLIT_ILP>(acc, inf, acc.z, tx, ty, take);
         // only the first nonzero digit of a lane starts from infinity: skip
         // the 24 selects in every window where no lane of the wave does
         if (__any(take && was_inf)) gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
@@ -629,7 +646,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
           fe az;
           fe_mul(az, acc.z, Zg);
           const bool was_inf = inf;
-          gej_accumulate(acc, inf, az, tx, ty, take);
+          ec_accumulate<SPLIT && HKV_SPLIT_ILP>(acc, inf, az, tx, ty, take);
           if (__any(take && was_inf)) {  // map the G-multiple onto the accumulator's curve
             fe zg2;
             fe_sqr(zg2, Zg);

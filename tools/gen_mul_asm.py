@@ -60,6 +60,157 @@ def column_block(k, pairs, name):
             f'      : {ins});')
 
 
+def column_block2(k, pairs1, pairs2):
+    """asm for column k of two independent products interleaved mad by mad:
+    %0 acc1, %1 top1, %2 acc2, %3 top2 (64-bit accs "+v", tops "=&v"),
+    %4 %5 carry pairs of product 1, %6 %7 of product 2, then the a/b regs
+    (names a*, b* for product 1 and c*, d* for product 2). A product's carry
+    is read >= 2 instructions after its mad (the other product's instructions
+    fill the gap that s_nop fills in the single form), so two rotating SGPR
+    pairs per product suffice."""
+    regs = {}
+    for (i, j) in pairs1:
+        for nm in (f"a{i}", f"b{j}"):
+            regs.setdefault(nm, len(regs))
+    for (i, j) in pairs2:
+        for nm in (f"c{i}", f"d{j}"):
+            regs.setdefault(nm, len(regs))
+    base = 8
+    ref = lambda nm: f"%{base + regs[nm]}"
+    streams = []
+    for q, (pairs, an, bn) in enumerate(((pairs1, "a", "b"), (pairs2, "c", "d"))):
+        seq = []
+        m = len(pairs)
+        for p in range(m):
+            seq.append(("mad", q, p, pairs[p], an, bn))
+            if p - 1 >= 0:
+                seq.append(("add", q, p - 1, None, an, bn))
+        if m:
+            seq.append(("add", q, m - 1, None, an, bn))
+        streams.append(seq)
+    # interleave the two streams item by item
+    merged = []
+    for x in range(max(len(streams[0]), len(streams[1]))):
+        for q in (0, 1):
+            if x < len(streams[q]):
+                merged.append(streams[q][x])
+    lines = []
+    emitted = {}
+    first_add = [True, True]
+    acc = ["%0", "%2"]
+    top = ["%1", "%3"]
+    for kind, q, p, pr, an, bn in merged:
+        c = f"%{4 + 2 * q + p % 2}"
+        if kind == "mad":
+            i, j = pr
+            lines.append(f"v_mad_u64_u32 {acc[q]}, {c}, {ref(an + str(i))}, {ref(bn + str(j))}, {acc[q]}")
+            emitted[(q, p)] = len(lines) - 1
+        else:
+            dist = len(lines) - 1 - emitted[(q, p)]
+            if dist < 2:
+                lines.append(f"s_nop {1 - dist}")
+            if first_add[q]:
+                lines.append(f"v_addc_co_u32_e64 {top[q]}, {c}, 0, 0, {c}")
+                first_add[q] = False
+            else:
+                lines.append(f"v_addc_co_u32_e64 {top[q]}, {c}, {top[q]}, 0, {c}")
+    asm = "\\n\\t".join(lines)
+    ins = ", ".join(f'"v"({nm[0]}[{nm[1:]}])' for nm in regs)
+    return (f'  asm("{asm}"\n      : "+v"(acc1), "=&v"(top1), "+v"(acc2), "=&v"(top2), "=&s"(c0), "=&s"(c1), "=&s"(e0), "=&s"(e1)\n'
+            f'      : {ins});')
+
+
+def pair_functions():
+    out = ["",
+           "// Two independent 256x256 products with their columns interleaved mad by",
+           "// mad: at one wave per SIMD (the small-batch split kernel) each mad's",
+           "// dependency latency is filled by the other product's instructions.",
+           "__device__ __forceinline__ void mul256_ps2(uint32_t t1[16], const uint32_t* a, const uint32_t* b,",
+           "                                           uint32_t t2[16], const uint32_t* c, const uint32_t* d) {",
+           "  uint64_t acc1 = 0, acc2 = 0;",
+           "  uint32_t top1, top2;",
+           "  uint64_t c0, c1, e0, e1;"]
+    for k in range(15):
+        pairs = [(i, k - i) for i in range(8) if 0 <= k - i < 8]
+        out.append(f"  // column {k}: 2 x {len(pairs)} products")
+        out.append(column_block2(k, pairs, pairs))
+        out.append(f"  t1[{k}] = (uint32_t)acc1;")
+        out.append(f"  t2[{k}] = (uint32_t)acc2;")
+        out.append("  acc1 = (acc1 >> 32) | ((uint64_t)top1 << 32);")
+        out.append("  acc2 = (acc2 >> 32) | ((uint64_t)top2 << 32);")
+    out.append("  t1[15] = (uint32_t)acc1;")
+    out.append("  t2[15] = (uint32_t)acc2;")
+    out.append("  (void)c0; (void)c1; (void)e0; (void)e1;")
+    out.append("}")
+    out.append("")
+    out.append("// 2*o + diagonal squares of one operand (the tail of a squaring)")
+    out.append("__device__ __forceinline__ void sqr_tail(uint32_t t[16], const uint32_t o[16], const uint32_t* a) {")
+    out.append("  uint32_t cy = 0;")
+    out.append("#pragma unroll")
+    out.append("  for (int i = 0; i < 8; ++i) {")
+    out.append("    const uint64_t dd = (uint64_t)a[i] * a[i];")
+    out.append("    const uint32_t s0 = (i == 0) ? (o[0] << 1) : __builtin_amdgcn_alignbit(o[2 * i], o[2 * i - 1], 31);")
+    out.append("    const uint32_t s1 = __builtin_amdgcn_alignbit(o[2 * i + 1], o[2 * i], 31);")
+    out.append("    t[2 * i] = __builtin_addc(s0, (uint32_t)dd, cy, &cy);")
+    out.append("    t[2 * i + 1] = __builtin_addc(s1, (uint32_t)(dd >> 32), cy, &cy);")
+    out.append("  }")
+    out.append("}")
+    out.append("")
+    out.append("// two independent squarings, off-diagonal scans interleaved")
+    out.append("__device__ __forceinline__ void sqr256_ps2(uint32_t t1[16], const uint32_t* a, uint32_t t2[16], const uint32_t* c) {")
+    out.append("  const uint32_t* b = a;")
+    out.append("  const uint32_t* d = c;")
+    out.append("  uint32_t o1[16], o2[16];")
+    out.append("  uint64_t acc1 = 0, acc2 = 0;")
+    out.append("  uint32_t top1, top2;")
+    out.append("  uint64_t c0, c1, e0, e1;")
+    out.append("  o1[0] = 0;")
+    out.append("  o2[0] = 0;")
+    for k in range(1, 14):
+        pairs = [(i, k - i) for i in range(8) if 0 <= k - i < 8 and i < k - i]
+        out.append(f"  // column {k}: 2 x {len(pairs)} off-diagonal products")
+        out.append(column_block2(k, pairs, pairs))
+        out.append(f"  o1[{k}] = (uint32_t)acc1;")
+        out.append(f"  o2[{k}] = (uint32_t)acc2;")
+        out.append("  acc1 = (acc1 >> 32) | ((uint64_t)top1 << 32);")
+        out.append("  acc2 = (acc2 >> 32) | ((uint64_t)top2 << 32);")
+    out.append("  o1[14] = (uint32_t)acc1;")
+    out.append("  o1[15] = (uint32_t)(acc1 >> 32);")
+    out.append("  o2[14] = (uint32_t)acc2;")
+    out.append("  o2[15] = (uint32_t)(acc2 >> 32);")
+    out.append("  (void)c0; (void)c1; (void)e0; (void)e1;")
+    out.append("  sqr_tail(t1, o1, a);")
+    out.append("  sqr_tail(t2, o2, c);")
+    out.append("}")
+    out.append("")
+    out.append("// a squaring (t1 = a^2) beside an independent product (t2 = c * d)")
+    out.append("__device__ __forceinline__ void sqrmul256_ps2(uint32_t t1[16], const uint32_t* a, uint32_t t2[16], const uint32_t* c,")
+    out.append("                                              const uint32_t* d) {")
+    out.append("  const uint32_t* b = a;")
+    out.append("  uint32_t o1[16];")
+    out.append("  uint64_t acc1 = 0, acc2 = 0;")
+    out.append("  uint32_t top1, top2;")
+    out.append("  uint64_t c0, c1, e0, e1;")
+    out.append("  o1[0] = 0;")
+    for k in range(15):
+        p1 = [(i, k - i) for i in range(8) if 0 <= k - i < 8 and i < k - i]
+        p2 = [(i, k - i) for i in range(8) if 0 <= k - i < 8]
+        out.append(f"  // column {k}: {len(p1)} off-diagonal + {len(p2)} products")
+        out.append(column_block2(k, p1, p2))
+        if 1 <= k <= 13:
+            out.append(f"  o1[{k}] = (uint32_t)acc1;")
+            out.append("  acc1 = (acc1 >> 32) | ((uint64_t)top1 << 32);")
+        out.append(f"  t2[{k}] = (uint32_t)acc2;")
+        out.append("  acc2 = (acc2 >> 32) | ((uint64_t)top2 << 32);")
+    out.append("  o1[14] = (uint32_t)acc1;")
+    out.append("  o1[15] = (uint32_t)(acc1 >> 32);")
+    out.append("  t2[15] = (uint32_t)acc2;")
+    out.append("  (void)c0; (void)c1; (void)e0; (void)e1;")
+    out.append("  sqr_tail(t1, o1, a);")
+    out.append("}")
+    return out
+
+
 def main():
     out = ["// GENERATED by tools/gen_mul_asm.py — do not edit.",
            "// 256x256 -> 512-bit product, product scanning in gfx950 inline asm",
@@ -115,6 +266,7 @@ def main():
     out.append("    t[2 * i + 1] = __builtin_addc(s1, d1, cy, &cy);")
     out.append("  }")
     out.append("}")
+    out.extend(pair_functions())
     out.append("")
     out.append("}  // namespace hkv")
     open(OUT, "w").write("\n".join(out) + "\n")

@@ -78,6 +78,12 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, S
     } else if constexpr (OP == 6) {
       bool hz, rz;
       gej_add_ge_core(p, p, p.z, b, p.y, hz, rz, nullptr);
+    } else if constexpr (OP == 11) {
+      fe_mul2(p.x, p.x, b, p.y, p.y, b);
+    } else if constexpr (OP == 12) {
+      fe_sqr2(p.x, p.x, p.y, p.y);
+    } else if constexpr (OP == 13) {
+      fe_sqrmul(p.x, p.x, p.y, p.y, b);
     } else if constexpr (OP == 7 || OP == 8 || OP == 9) {
       fe29::fe a29, b29;
 #pragma unroll
@@ -117,7 +123,8 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, S
 
 static const char* NAMES[] = {"fe_mul", "fe_sqr", "fe_mul x2 (independent)", "fe_add", "fe_sub", "gej_double",
                               "gej_add_ge (mixed)", "fe29_mul", "fe29_sqr", "fe29_sub+carry",
-                              "fp52_mul (product only, lower bound)"};
+                              "fp52_mul (product only, lower bound)", "fe_mul2 (interleaved pair)",
+                              "fe_sqr2 (interleaved pair)", "fe_sqrmul (interleaved pair)"};
 
 template <int OP>
 void run(int n_cu, int blocks_per_cu) {
@@ -158,14 +165,57 @@ void run(int n_cu, int blocks_per_cu) {
   hipFree(st);
 }
 
+// paired forms against the single forms on pseudo-random operands (including
+// values >= p, the weak form the kernels carry)
+__global__ void check_pairs(uint32_t* bad) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  fe a, b, c, d;
+  uint32_t x = tid * 0x9E3779B9u + 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5; a.v[k] = x;
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5; b.v[k] = x;
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5; c.v[k] = x;
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5; d.v[k] = x;
+  }
+  if (tid % 7 == 0) for (int k = 0; k < 8; ++k) a.v[k] = 0xFFFFFFFFu;
+  if (tid % 11 == 0) for (int k = 0; k < 8; ++k) c.v[k] = 0xFFFFFFFFu;
+  fe r1, r2, s1, s2;
+  uint32_t nb = 0;
+  fe_mul2(r1, a, b, r2, c, d);
+  fe_mul(s1, a, b); fe_mul(s2, c, d);
+  fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
+  nb += !fe_eq_norm(r1, s1) + !fe_eq_norm(r2, s2);
+  fe_sqr2(r1, a, r2, c);
+  fe_sqr(s1, a); fe_sqr(s2, c);
+  fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
+  nb += !fe_eq_norm(r1, s1) + !fe_eq_norm(r2, s2);
+  fe_sqrmul(r1, a, r2, c, d);
+  fe_sqr(s1, a); fe_mul(s2, c, d);
+  fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
+  nb += !fe_eq_norm(r1, s1) + !fe_eq_norm(r2, s2);
+  if (nb) atomicAdd(bad, nb);
+}
+
 int main() {
   hipDeviceProp_t p;
   hipGetDeviceProperties(&p, 0);
   const int n_cu = p.multiProcessorCount;
+  {
+    uint32_t* bad;
+    hipMalloc(&bad, 4);
+    hipMemset(bad, 0, 4);
+    hipLaunchKernelGGL(check_pairs, dim3(1024), dim3(256), 0, 0, bad);
+    uint32_t hb = 0;
+    hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
+    printf("{\"check\": \"paired field ops vs single\", \"lanes\": %d, \"mismatches\": %u}\n", 1024 * 256, hb);
+    hipFree(bad);
+  }
   for (int bpc : {1, 2, 4}) {
     run<0>(n_cu, bpc); run<1>(n_cu, bpc); run<2>(n_cu, bpc); run<3>(n_cu, bpc);
     run<4>(n_cu, bpc); run<5>(n_cu, bpc); run<6>(n_cu, bpc);
     run<7>(n_cu, bpc); run<8>(n_cu, bpc); run<9>(n_cu, bpc); run<10>(n_cu, bpc);
+    run<11>(n_cu, bpc); run<12>(n_cu, bpc); run<13>(n_cu, bpc);
   }
   return 0;
 }
