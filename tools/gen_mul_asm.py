@@ -211,6 +211,298 @@ def pair_functions():
     return out
 
 
+def scan_block(pairs, mode):
+    """asm for one column of the reduced scan (mul256_red_ps / sqr256_red_ps).
+
+    pairs: [(x, y)] C expressions of the 32-bit limb operands of the column's
+    products. mode:
+      "acc"  -- acc is "+v" (C-level carry-in, as in column_block)
+      "red0" -- low column 0: acc = h0 * 977 (no carry-in)
+      "red"  -- low column j >= 1: acc = prevhi + init, init = (top_prev << 32) | h[j-1],
+                then acc += h[j] * 977. Both sums stay below 2^43, so their
+                carry-outs are discarded (written to %2 before any product).
+    Operands: %0 acc, %1 top, %2..%4 carry pairs; then (red modes) the prefix
+    operands; then the limb operands."""
+    regs = {}
+    for (x, y) in pairs:
+        for nm in (x, y):
+            regs.setdefault(nm, len(regs))
+    lines = []
+    if mode == "acc":
+        pre_ins = []
+    elif mode == "red0":
+        pre_ins = ['"v"(h[0])', '"s"(k977)']
+        lines.append("v_mad_u64_u32 %0, %2, %5, %6, 0")
+    else:
+        pre_ins = ['"v"(prevhi)', '"v"(init)', '"v"(hj)', '"s"(k977)']
+        lines.append("v_mad_u64_u32 %0, %2, %5, 1, %6")
+        lines.append("v_mad_u64_u32 %0, %2, %7, %8, %0")
+    base = 5 + len(pre_ins)
+    ref = lambda nm: f"%{base + regs[nm]}"
+    m = len(pairs)
+    seq = []
+    for p in range(m):
+        seq.append(("mad", p))
+        if p - 2 >= 0:
+            seq.append(("add", p - 2))
+    for p in range(max(0, m - 2), m):
+        seq.append(("add", p))
+    emitted_mad = {}
+    first_add = True
+    for kind, p in seq:
+        c = f"%{2 + p % 3}"
+        if kind == "mad":
+            x, y = pairs[p]
+            lines.append(f"v_mad_u64_u32 %0, {c}, {ref(x)}, {ref(y)}, %0")
+            emitted_mad[p] = len(lines) - 1
+        else:
+            dist = len(lines) - 1 - emitted_mad[p]
+            if dist < 2:
+                lines.append(f"s_nop {1 - dist}")
+            if first_add:
+                lines.append(f"v_addc_co_u32_e64 %1, {c}, 0, 0, {c}")
+                first_add = False
+            else:
+                lines.append(f"v_addc_co_u32_e64 %1, {c}, %1, 0, {c}")
+    asm = "\\n\\t".join(lines)
+    accc = '"+v"(acc)' if mode == "acc" else '"=&v"(accn)'
+    ins = ", ".join(pre_ins + [f'"v"({nm})' for nm in regs])
+    return (f'  asm("{asm}"\n      : {accc}, "=&v"(top), "=&s"(c0), "=&s"(c1), "=&s"(c2)\n'
+            f'      : {ins});')
+
+
+def reduced_scan(name, cols, doc):
+    """A 256x256 product given as column pair lists cols[0..14], reduced mod p
+    on the fly: columns 8..14 are scanned first (their carry-in from column 7
+    is deferred), giving the high half h[0..7]; columns 0..7 then fold
+    h * 2^256 == h * (2^32 + 977) into their accumulators (h[j] * 977 and
+    h[j-1] enter column j). Output: r[0..7] and T < 2^38 with
+    a * b == r + T * 2^256 (mod p)."""
+    out = [""] + ["// " + l for l in doc] + [
+        f"__device__ __forceinline__ void {name}(uint32_t r[8], uint64_t& T, const uint32_t* a, const uint32_t* b) {{",
+        "  uint64_t acc = 0;",
+        "  uint32_t top;",
+        "  uint64_t c0, c1, c2;",
+        "  uint32_t h[8], o[8];",
+        "  const uint32_t k977 = 977u;"]
+    if "sqr" in name:
+        out += ["  (void)b;",
+                "  // row i of the square multiplies a_i by X_i = a_i + 2 * sum_{j>i} a_j 2^(32(j-i)),",
+                "  // whose limbs are a_i, e[i+1] = a_{i+1} << 1, then d[i+k] = (a_{i+k} << 1) | (a_{i+k-1} >> 31)",
+                "  uint32_t e[8], d[9];",
+                "#pragma unroll",
+                "  for (int j = 1; j < 8; ++j) e[j] = a[j] << 1;",
+                "#pragma unroll",
+                "  for (int j = 2; j < 8; ++j) d[j] = __builtin_amdgcn_alignbit(a[j], a[j - 1], 31);",
+                "  d[8] = a[7] >> 31;"]
+    for k in range(8, 15):
+        out.append(f"  // column {k}: {len(cols[k])} products")
+        out.append(scan_block(cols[k], "acc"))
+        out.append(f"  h[{k - 8}] = (uint32_t)acc;")
+        out.append("  acc = (acc >> 32) | ((uint64_t)top << 32);")
+    out.append("  h[7] = (uint32_t)acc;  // the high half is < 2^256: nothing above")
+    for j in range(8):
+        out.append(f"  // column {j}: {len(cols[j])} products + h[{j}] * 977" + (f" + h[{j - 1}]" if j else ""))
+        out.append("  {")
+        out.append("    uint64_t accn;")
+        if j:
+            out.append("    const uint32_t prevhi = (uint32_t)(acc >> 32);")
+            out.append(f"    const uint64_t init = ((uint64_t)top << 32) | h[{j - 1}];")
+            out.append(f"    const uint32_t hj = h[{j}];")
+            blk = scan_block(cols[j], "red")
+        else:
+            blk = scan_block(cols[j], "red0")
+        out.append("  " + blk.replace("\n", "\n  "))
+        out.append("    acc = accn;")
+        out.append("  }")
+        out.append(f"  o[{j}] = (uint32_t)acc;")
+    out.append("  T = (acc >> 32) + ((uint64_t)top << 32) + h[7];")
+    out.append("  // r may alias a or b (fe_mul(x, x, y)): written only after the last column")
+    out.append("#pragma unroll")
+    out.append("  for (int j = 0; j < 8; ++j) r[j] = o[j];")
+    out.append("  (void)c0; (void)c1; (void)c2;")
+    out.append("}")
+    return out
+
+
+def reduced_functions():
+    mul_cols = [[(f"a[{i}]", f"b[{k - i}]") for i in range(8) if 0 <= k - i < 8] for k in range(15)]
+    sqr_cols = [[] for _ in range(16)]
+    for i in range(8):
+        sqr_cols[2 * i].append((f"a[{i}]", f"a[{i}]"))
+        if i <= 6:
+            sqr_cols[2 * i + 1].append((f"a[{i}]", f"e[{i + 1}]"))
+        for j in range(i + 2, 9):
+            sqr_cols[i + j].append((f"a[{i}]", f"d[{j}]"))
+    assert not sqr_cols[15] and sum(map(len, sqr_cols)) == 43
+    out = reduced_scan("mul256_red_ps", mul_cols, [
+        "a * b mod p with the reduction folded into the product scan (HKV_MUL_RED):",
+        "no separate 8-mad reduction chain, its limb moves or its two 8-limb",
+        "add chains; a column's carry-in and h[j-1] enter through one mad (x 1)."])
+    out += reduced_scan("sqr256_red_ps", sqr_cols[:15], [
+        "a^2 mod p as a column scan of 43 products (8 squares, 7 a_i * 2a_{i+1},",
+        "28 a_i * (2a)_j limbs incl. the 1-bit limb 8) instead of 36 products plus",
+        "a shift-and-add pass over 16 words, with the same folded reduction."])
+    return out
+
+
+def scan_block2(pairs1, pairs2, mode):
+    """Two reduced-scan columns (scan_block) interleaved mad by mad, for the
+    paired forms. %0 acc1, %1 top1, %2 acc2, %3 top2, %4 %5 carry pairs of
+    stream 1, %6 %7 of stream 2, then the prefix operands of both streams
+    (red modes), then the limb operands."""
+    regs = {}
+    for (x, y) in pairs1 + pairs2:
+        for nm in (x, y):
+            regs.setdefault(nm, len(regs))
+    lines = []
+    if mode == "acc":
+        pre_ins = []
+    elif mode == "red0":
+        pre_ins = ['"v"(h1[0])', '"v"(h2[0])', '"s"(k977)']
+        lines.append("v_mad_u64_u32 %0, %4, %8, %10, 0")
+        lines.append("v_mad_u64_u32 %2, %6, %9, %10, 0")
+    else:
+        pre_ins = ['"v"(prevhi1)', '"v"(init1)', '"v"(hj1)', '"v"(prevhi2)', '"v"(init2)', '"v"(hj2)', '"s"(k977)']
+        lines.append("v_mad_u64_u32 %0, %4, %8, 1, %9")
+        lines.append("v_mad_u64_u32 %2, %6, %11, 1, %12")
+        lines.append("v_mad_u64_u32 %0, %4, %10, %14, %0")
+        lines.append("v_mad_u64_u32 %2, %6, %13, %14, %2")
+    base = 8 + len(pre_ins)
+    ref = lambda nm: f"%{base + regs[nm]}"
+    streams = []
+    for q, pairs in enumerate((pairs1, pairs2)):
+        seq = []
+        m = len(pairs)
+        for p in range(m):
+            seq.append(("mad", q, p, pairs[p]))
+            if p - 1 >= 0:
+                seq.append(("add", q, p - 1, None))
+        if m:
+            seq.append(("add", q, m - 1, None))
+        streams.append(seq)
+    merged = []
+    for x in range(max(len(streams[0]), len(streams[1]))):
+        for q in (0, 1):
+            if x < len(streams[q]):
+                merged.append(streams[q][x])
+    emitted = {}
+    first_add = [True, True]
+    acc = ["%0", "%2"]
+    top = ["%1", "%3"]
+    for kind, q, p, pr in merged:
+        c = f"%{4 + 2 * q + p % 2}"
+        if kind == "mad":
+            x, y = pr
+            lines.append(f"v_mad_u64_u32 {acc[q]}, {c}, {ref(x)}, {ref(y)}, {acc[q]}")
+            emitted[(q, p)] = len(lines) - 1
+        else:
+            dist = len(lines) - 1 - emitted[(q, p)]
+            if dist < 2:
+                lines.append(f"s_nop {1 - dist}")
+            if first_add[q]:
+                lines.append(f"v_addc_co_u32_e64 {top[q]}, {c}, 0, 0, {c}")
+                first_add[q] = False
+            else:
+                lines.append(f"v_addc_co_u32_e64 {top[q]}, {c}, {top[q]}, 0, {c}")
+    asm = "\\n\\t".join(lines)
+    accc = '"+v"(acc1), "=&v"(top1), "+v"(acc2), "=&v"(top2)' if mode == "acc" else \
+        '"=&v"(accn1), "=&v"(top1), "=&v"(accn2), "=&v"(top2)'
+    ins = ", ".join(pre_ins + [f'"v"({nm})' for nm in regs])
+    return (f'  asm("{asm}"\n      : {accc}, "=&s"(c0), "=&s"(c1), "=&s"(e0), "=&s"(e1)\n'
+            f'      : {ins});')
+
+
+def sqr_prep(src, e, d):
+    return [f"  uint32_t {e}[8], {d}[9];",
+            "#pragma unroll",
+            f"  for (int j = 1; j < 8; ++j) {e}[j] = {src}[j] << 1;",
+            "#pragma unroll",
+            f"  for (int j = 2; j < 8; ++j) {d}[j] = __builtin_amdgcn_alignbit({src}[j], {src}[j - 1], 31);",
+            f"  {d}[8] = {src}[7] >> 31;"]
+
+
+def reduced_scan2(name, sig, cols1, cols2, preps, doc):
+    out = [""] + ["// " + l for l in doc] + [
+        f"__device__ __forceinline__ void {name}({sig}) {{",
+        "  uint64_t acc1 = 0, acc2 = 0;",
+        "  uint32_t top1, top2;",
+        "  uint64_t c0, c1, e0, e1;",
+        "  uint32_t h1[8], h2[8], o1[8], o2[8];",
+        "  const uint32_t k977 = 977u;"]
+    for pr in preps:
+        out += sqr_prep(*pr)
+    for k in range(8, 15):
+        out.append(f"  // column {k}: {len(cols1[k])} + {len(cols2[k])} products")
+        out.append(scan_block2(cols1[k], cols2[k], "acc"))
+        out.append(f"  h1[{k - 8}] = (uint32_t)acc1;")
+        out.append(f"  h2[{k - 8}] = (uint32_t)acc2;")
+        out.append("  acc1 = (acc1 >> 32) | ((uint64_t)top1 << 32);")
+        out.append("  acc2 = (acc2 >> 32) | ((uint64_t)top2 << 32);")
+    out.append("  h1[7] = (uint32_t)acc1;")
+    out.append("  h2[7] = (uint32_t)acc2;")
+    for j in range(8):
+        out.append(f"  // column {j}: {len(cols1[j])} + {len(cols2[j])} products + the folded high limbs")
+        out.append("  {")
+        out.append("    uint64_t accn1, accn2;")
+        if j:
+            for q in (1, 2):
+                out.append(f"    const uint32_t prevhi{q} = (uint32_t)(acc{q} >> 32);")
+                out.append(f"    const uint64_t init{q} = ((uint64_t)top{q} << 32) | h{q}[{j - 1}];")
+                out.append(f"    const uint32_t hj{q} = h{q}[{j}];")
+            blk = scan_block2(cols1[j], cols2[j], "red")
+        else:
+            blk = scan_block2(cols1[j], cols2[j], "red0")
+        out.append("  " + blk.replace("\n", "\n  "))
+        out.append("    acc1 = accn1;")
+        out.append("    acc2 = accn2;")
+        out.append("  }")
+        out.append(f"  o1[{j}] = (uint32_t)acc1;")
+        out.append(f"  o2[{j}] = (uint32_t)acc2;")
+    out.append("  T1 = (acc1 >> 32) + ((uint64_t)top1 << 32) + h1[7];")
+    out.append("  T2 = (acc2 >> 32) + ((uint64_t)top2 << 32) + h2[7];")
+    out.append("#pragma unroll")
+    out.append("  for (int j = 0; j < 8; ++j) { r1[j] = o1[j]; r2[j] = o2[j]; }")
+    out.append("  (void)c0; (void)c1; (void)e0; (void)e1;")
+    out.append("}")
+    return out
+
+
+def col_lists(kind, x, y=None):
+    if kind == "mul":
+        return [[(f"{x}[{i}]", f"{y}[{k - i}]") for i in range(8) if 0 <= k - i < 8] for k in range(15)]
+    e, d = y
+    cols = [[] for _ in range(16)]
+    for i in range(8):
+        cols[2 * i].append((f"{x}[{i}]", f"{x}[{i}]"))
+        if i <= 6:
+            cols[2 * i + 1].append((f"{x}[{i}]", f"{e}[{i + 1}]"))
+        for j in range(i + 2, 9):
+            cols[i + j].append((f"{x}[{i}]", f"{d}[{j}]"))
+    return cols[:15]
+
+
+def reduced_pair_functions():
+    out = reduced_scan2(
+        "mul256_red_ps2",
+        "uint32_t r1[8], uint64_t& T1, const uint32_t* a, const uint32_t* b, uint32_t r2[8], uint64_t& T2, "
+        "const uint32_t* c, const uint32_t* d",
+        col_lists("mul", "a", "b"), col_lists("mul", "c", "d"), [],
+        ["two independent folded-reduction products (mul256_red_ps) interleaved mad by mad"])
+    out += reduced_scan2(
+        "sqr256_red_ps2",
+        "uint32_t r1[8], uint64_t& T1, const uint32_t* a, uint32_t r2[8], uint64_t& T2, const uint32_t* c",
+        col_lists("sqr", "a", ("ea", "da")), col_lists("sqr", "c", ("ec", "dc")), [("a", "ea", "da"), ("c", "ec", "dc")],
+        ["two independent folded-reduction squares (sqr256_red_ps) interleaved mad by mad"])
+    out += reduced_scan2(
+        "sqrmul256_red_ps2",
+        "uint32_t r1[8], uint64_t& T1, const uint32_t* a, uint32_t r2[8], uint64_t& T2, const uint32_t* c, "
+        "const uint32_t* d",
+        col_lists("sqr", "a", ("ea", "da")), col_lists("mul", "c", "d"), [("a", "ea", "da")],
+        ["a folded-reduction square beside an independent product, interleaved mad by mad"])
+    return out
+
+
 def main():
     out = ["// GENERATED by tools/gen_mul_asm.py — do not edit.",
            "// 256x256 -> 512-bit product, product scanning in gfx950 inline asm",
@@ -267,6 +559,8 @@ def main():
     out.append("  }")
     out.append("}")
     out.extend(pair_functions())
+    out.extend(reduced_functions())
+    out.extend(reduced_pair_functions())
     out.append("")
     out.append("}  // namespace hkv")
     open(OUT, "w").write("\n".join(out) + "\n")

@@ -84,6 +84,10 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, S
       fe_sqr2(p.x, p.x, p.y, p.y);
     } else if constexpr (OP == 13) {
       fe_sqrmul(p.x, p.x, p.y, p.y, b);
+    } else if constexpr (OP == 14) {
+      fe_mul_ref(p.x, p.x, b);
+    } else if constexpr (OP == 15) {
+      fe_sqr_ref(p.x, p.x);
     } else if constexpr (OP == 7 || OP == 8 || OP == 9) {
       fe29::fe a29, b29;
 #pragma unroll
@@ -124,7 +128,8 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out, S
 static const char* NAMES[] = {"fe_mul", "fe_sqr", "fe_mul x2 (independent)", "fe_add", "fe_sub", "gej_double",
                               "gej_add_ge (mixed)", "fe29_mul", "fe29_sqr", "fe29_sub+carry",
                               "fp52_mul (product only, lower bound)", "fe_mul2 (interleaved pair)",
-                              "fe_sqr2 (interleaved pair)", "fe_sqrmul (interleaved pair)"};
+                              "fe_sqr2 (interleaved pair)", "fe_sqrmul (interleaved pair)",
+                              "fe_mul_ref (512-bit product + fe_reduce512)", "fe_sqr_ref (512-bit square + fe_reduce512)"};
 
 template <int OP>
 void run(int n_cu, int blocks_per_cu) {
@@ -165,6 +170,51 @@ void run(int n_cu, int blocks_per_cu) {
   hipFree(st);
 }
 
+// fe_inv through the reference (512-bit product) ops: the same addition chain
+__device__ void fe_inv_ref(fe& r, const fe& a) {
+  fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  auto sqn = [](fe& o, const fe& i, int n) { fe_sqr_ref(o, i); for (int k = 1; k < n; ++k) fe_sqr_ref(o, o); };
+  fe_sqr_ref(x2, a); fe_mul_ref(x2, x2, a);
+  fe_sqr_ref(x3, x2); fe_mul_ref(x3, x3, a);
+  sqn(t, x3, 3); fe_mul_ref(x6, t, x3);
+  sqn(t, x6, 3); fe_mul_ref(x9, t, x3);
+  sqn(t, x9, 2); fe_mul_ref(x11, t, x2);
+  sqn(t, x11, 11); fe_mul_ref(x22, t, x11);
+  sqn(t, x22, 22); fe_mul_ref(x44, t, x22);
+  sqn(t, x44, 44); fe_mul_ref(x88, t, x44);
+  sqn(t, x88, 88); fe_mul_ref(x176, t, x88);
+  sqn(t, x176, 44); fe_mul_ref(x220, t, x44);
+  sqn(t, x220, 3); fe_mul_ref(x223, t, x3);
+  sqn(t, x223, 23); fe_mul_ref(t, t, x22);
+  sqn(t, t, 5); fe_mul_ref(t, t, a);
+  sqn(t, t, 3); fe_mul_ref(t, t, x2);
+  sqn(t, t, 2); fe_mul_ref(r, t, a);
+}
+
+// chains: fe_inv and 64 squarings with the kernels' ops against the reference ops
+__global__ void check_chains(uint32_t* bad) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  fe a;
+  uint32_t x = tid * 0x85EBCA6Bu + 7;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; a.v[k] = x; }
+  fe r, s;
+  uint32_t nb = 0;
+  fe_inv(r, a); fe_inv_ref(s, a);
+  fe_normalize(r); fe_normalize(s);
+  nb += !fe_eq_norm(r, s);
+  fe_sqr_n(r, a, 64);
+  s = a;
+  for (int k = 0; k < 64; ++k) fe_sqr_ref(s, s);
+  fe_normalize(r); fe_normalize(s);
+  nb += 2 * !fe_eq_norm(r, s);
+  fe_mul(r, a, a); fe_mul(r, r, a); fe_sqr(r, r); fe_mul(r, a, r);
+  fe_mul_ref(s, a, a); fe_mul_ref(s, s, a); fe_sqr_ref(s, s); fe_mul_ref(s, a, s);
+  fe_normalize(r); fe_normalize(s);
+  nb += 4 * !fe_eq_norm(r, s);
+  if (nb) atomicOr(bad, nb);
+}
+
 // paired forms against the single forms on pseudo-random operands (including
 // values >= p, the weak form the kernels carry)
 __global__ void check_pairs(uint32_t* bad) {
@@ -180,8 +230,26 @@ __global__ void check_pairs(uint32_t* bad) {
   }
   if (tid % 7 == 0) for (int k = 0; k < 8; ++k) a.v[k] = 0xFFFFFFFFu;
   if (tid % 11 == 0) for (int k = 0; k < 8; ++k) c.v[k] = 0xFFFFFFFFu;
+  if (tid % 13 == 0) for (int k = 0; k < 8; ++k) b.v[k] = 0xFFFFFFFFu;
+  if (tid % 17 == 0) { for (int k = 0; k < 8; ++k) a.v[k] = 0; a.v[0] = tid & 3; }
+  if (tid % 19 == 0) { a.v[0] = 0xFFFFFC2Fu; a.v[1] = 0xFFFFFFFEu; for (int k = 2; k < 8; ++k) a.v[k] = 0xFFFFFFFFu; }
+  if (tid % 23 == 0) for (int k = 0; k < 8; ++k) a.v[k] = (k & 1) ? 0x80000000u : 0xFFFFFFFFu;
   fe r1, r2, s1, s2;
   uint32_t nb = 0;
+  // folded-reduction forms (fe_mul / fe_sqr) against the 512-bit product path
+  fe_mul(r1, a, b); fe_mul_ref(s1, a, b);
+  fe_sqr(r2, a); fe_sqr_ref(s2, a);
+  fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
+  nb += !fe_eq_norm(r1, s1) + !fe_eq_norm(r2, s2);
+  fe_mul(r1, c, d); fe_mul_ref(s1, c, d);
+  fe_sqr(r2, c); fe_sqr_ref(s2, c);
+  fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
+  nb += !fe_eq_norm(r1, s1) + !fe_eq_norm(r2, s2);
+  // in place, as the kernels call them
+  r1 = a; fe_mul(r1, r1, b); fe_mul_ref(s1, a, b);
+  r2 = c; fe_sqr(r2, r2); fe_sqr_ref(s2, c);
+  fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
+  nb += !fe_eq_norm(r1, s1) + !fe_eq_norm(r2, s2);
   fe_mul2(r1, a, b, r2, c, d);
   fe_mul(s1, a, b); fe_mul(s2, c, d);
   fe_normalize(r1); fe_normalize(r2); fe_normalize(s1); fe_normalize(s2);
@@ -208,7 +276,11 @@ int main() {
     hipLaunchKernelGGL(check_pairs, dim3(1024), dim3(256), 0, 0, bad);
     uint32_t hb = 0;
     hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
-    printf("{\"check\": \"paired field ops vs single\", \"lanes\": %d, \"mismatches\": %u}\n", 1024 * 256, hb);
+    printf("{\"check\": \"paired and folded-reduction field ops vs the 512-bit path\", \"lanes\": %d, \"mismatches\": %u}\n", 1024 * 256, hb);
+    hipMemset(bad, 0, 4);
+    hipLaunchKernelGGL(check_chains, dim3(64), dim3(256), 0, 0, bad);
+    hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
+    printf("{\"check\": \"fe_inv / 64 squarings / mixed chain vs the reference ops (bit mask of failing checks)\", \"lanes\": %d, \"fail_mask\": %u}\n", 64 * 256, hb);
     hipFree(bad);
   }
   for (int bpc : {1, 2, 4}) {
@@ -216,6 +288,7 @@ int main() {
     run<4>(n_cu, bpc); run<5>(n_cu, bpc); run<6>(n_cu, bpc);
     run<7>(n_cu, bpc); run<8>(n_cu, bpc); run<9>(n_cu, bpc); run<10>(n_cu, bpc);
     run<11>(n_cu, bpc); run<12>(n_cu, bpc); run<13>(n_cu, bpc);
+    run<14>(n_cu, bpc); run<15>(n_cu, bpc);
   }
   return 0;
 }
