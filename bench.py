@@ -13,9 +13,9 @@ plus, for N > 1, the RCCL all-gather of the verdict bitmap (the only
 collective; hkv/shard.py ShardedVerify). value = all ranks' verifies /
 max-over-ranks time.
 
-Also reported (rank 0, N = 1): the ecmult kernel's roofline (the REFERENCE
+Also reported (rank 0, N = 1): the ecmult stage's roofline (the REFERENCE
 algorithm's limb products per verify, hkv/opcount.py P_ALG_ECMULT, over the
-HIP-event-timed launch, against the v_mad_u64_u32 peak at 2.4 GHz and at the
+HIP-event-timed ecmult + finish launches, against the v_mad_u64_u32 peak at 2.4 GHz and at the
 measured mad rate and clock); configs[0] (the 2,000-tx P2PKH block), [2]
 (block mix) and [3] (adversarial 1M, every class of hkv/adversarial.py); and
 the CPU baseline leg: the C restatement (oracle/, kind "port") and OpenSSL's
@@ -543,7 +543,8 @@ def main() -> None:
             "roofline": {"bound": "valu_int", "achieved": round(achieved, 4), "peak": round(peak, 3),
                          "unit": "T limb-products/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
                          "traffic": traffic,
-                         "kernel": "hkv_ecmult_kernel",
+                         "kernel": "ecmult stage: hkv_ecmult_kernel (u2*Q on E_w) + hkv_finish_kernel (u1*G, "
+                                   "num/den) + hkv_rare_kernel + hkv_yverdict_kernel (den^-1, y_c^2 == w)",
                          "p_alg": opcount.P_ALG_ECMULT,
                          "p_alg_note": "reference algorithm (libsecp256k1 ecmult: GLV + wNAF5 Q, w=15 G tables, "
                                        "129 doublings) priced in 32x32 limb products; frozen (hkv/opcount.py)",

@@ -150,16 +150,24 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
 #ifndef HKV_PROLOGUE_SPLIT
 #define HKV_PROLOGUE_SPLIT 1
 #endif
+#if HKV_YFREE && !HKV_PROLOGUE_SPLIT
+#error "y-free: the split ecmult reads y from the one-launch prologue (the three-kernel prologue leaves w)"
+#endif
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
   HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
           "prologue launch");
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
-  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, out_bits ? out_bits : d.bits,
-                             (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32), split, d.profile ? d.clk : nullptr,
-                             st),
+  uint32_t* vbits = out_bits ? out_bits : d.bits;
+  const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
+  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split,
+                             d.profile ? d.clk : nullptr, st),
           "ecmult launch");
+  // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
+  // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)
+  if (!split && HKV_YFREE) HKV_TRY(hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, vbits, n_words, st),
+                                   "finish launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
     d.ev.insert(d.ev.end(), e, e + 3);
@@ -193,7 +201,7 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
   HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
-  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 64 MiB at radix 2^20
+  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 448 MiB at radix 2^20 (y-free)
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
   if (per_cu < 1) per_cu = 1;

@@ -95,6 +95,38 @@ HKV_DEV bool pubkey_parse_rec(const uint32_t* w, fe& x, fe& y) {
   }
   return pk_ok;
 }
+// The y-free form of the parse (HKV_YFREE): the same accept rules except the
+// one that needs the square root — x^3 + 7 of a compressed key is not shown
+// to be a square here; the finish kernels' y_c^2 == w test rejects a
+// non-square (no y_c exists), and their rare paths test it explicitly.
+// Outputs x, w = x^3 + 7 (normalised) and FLAG_YODD / FLAG_COMP.
+HKV_DEV bool pubkey_parse_rec_w(const uint32_t* w, fe& x, fe& rhs, uint32_t& pflags) {
+  const uint32_t pklen = w[24] & 0xFFu;
+  const uint32_t prefix = (w[24] >> 8) & 0xFFu;
+  const bool comp = (pklen == 33u) && (prefix == 2u || prefix == 3u);
+  const bool unc = (pklen == 65u) && (prefix == 4u || prefix == 6u || prefix == 7u);
+  fe y, t;
+  rec_be256(x.v, w, 98);
+  rec_be256(y.v, w, 130);
+  bool pk_ok = (comp || unc) && u256_lt_p(x.v);
+  if (unc) pk_ok = pk_ok && u256_lt_p(y.v);
+  fe_sqr(t, x);
+  fe_mul(t, t, x);
+  fe seven;
+  fe_set_u32(seven, 7);
+  fe_add(rhs, t, seven);
+  fe_normalize(rhs);
+  if (unc) {
+    fe y2;
+    fe_sqr(y2, y);
+    pk_ok = pk_ok && fe_equal(y2, rhs);
+    if (prefix != 4u) pk_ok = pk_ok && ((y.v[0] & 1u) == (prefix & 1u));  // hybrid parity
+  }
+  const bool yodd = comp ? (prefix & 1u) != 0 : (y.v[0] & 1u) != 0;
+  pflags = (yodd ? FLAG_YODD : 0u) | (comp ? FLAG_COMP : 0u);
+  return pk_ok;
+}
+
 __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(const uint32_t* __restrict__ recs, uint32_t n,
                                                           uint32_t n_pad, uint32_t mode,
                                                           uint32_t* __restrict__ im) {
@@ -131,11 +163,16 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(co
   ok = ok && !u256_is_zero(r.v) && !u256_is_zero(s.v);
   sc_cond_sub_n(m.v);  // m = msg32 mod n (msg32 < 2^256 < 2n)
 
-  // --- pubkey: secp256k1_ec_pubkey_parse
+  // --- pubkey: secp256k1_ec_pubkey_parse (y-free: y stays implicit, IM_QY = w)
   fe x, y;
+  uint32_t pflags = 0;
+#if HKV_YFREE
+  ok = pubkey_parse_rec_w(w, x, y, pflags) && ok;
+#else
   ok = pubkey_parse_rec(w, x, y) && ok;
+#endif
 
-  const uint32_t flags = ok ? FLAG_VALID : 0u;
+  const uint32_t flags = (ok ? FLAG_VALID : 0u) | pflags;
   im[(size_t)IM_FLAGS * n_pad + i] = flags;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -450,7 +487,7 @@ HKV_DEV void ec_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, cons
 }
 
 template <bool SPLIT>
-__global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(const uint32_t* __restrict__ im, uint32_t n,
+__global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits, uint32_t n_words,
@@ -488,6 +525,15 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
       q.x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
       q.y.v[k] = im[(size_t)(IM_QY + k) * n_pad + i];
     }
+#if HKV_YFREE
+    if (!SPLIT) {  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
+      fe xw, ww;
+      fe_mul(xw, q.x, q.y);
+      fe_sqr(ww, q.y);
+      q.x = xw;
+      q.y = ww;
+    }
+#endif
     if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
     const bool neg1 = (flags & FLAG_NEG1) != 0, neg2 = (flags & FLAG_NEG2) != 0;
 
@@ -574,7 +620,8 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
       const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
       const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
-      const bool gwin = (win % GSTEP) == 0;
+      // y-free full-grid launches leave u1 * G to the finish kernel
+      const bool gwin = (SPLIT || !HKV_YFREE) && (win % GSTEP) == 0;
       uint32_t gd0 = 0, gd1 = 0;
       if (gwin) {
         const int gj = win / GSTEP;
@@ -705,6 +752,20 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
       __syncthreads();  // the next window loop's G DMA reuses gpf
     }
 
+#if HKV_YFREE
+    if (!SPLIT) {  // hand B' = (X, Y, Z acc * Zg) on E_w to the finish kernel
+      fe zt;
+      fe_mul(zt, acc.z, Zg);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
+        im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
+        im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
+      }
+      im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
+      continue;
+    }
+#endif
     // ---- inversion-free x compare ----
     bool accept = false;
     {
@@ -745,6 +806,306 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
     clk[3] = wall_clock64();
   }
 }
+
+#if HKV_YFREE
+// ---------------------------------------------------------------------------
+// 2b. y-free finish (full-grid batches). The ecmult kernel leaves
+//   B' = u2 * Q' = (X, Y, Z) on E_w : y^2 = x^3 + 7 w^3, Q' = (x w, w^2) =
+//   phi(Q) for the isomorphism phi(x, y) = (y0^2 x, y0^3 y), y0 = the key's y,
+//   so B = u2 * Q = (X / (Z^2 w), Y y0 / (Z^3 w^2)) is linear in y0. With
+//   A = u1 * G = (XA, YA, ZA), the affine sum's x is K1 - K2 y0, and
+//   "x(A + B) == r" solves to y0 = num / den with
+//     num = Y^2 ZA^6 + YA^2 Z^6 w^3 - H^2 (r T + XA Z^2 w + X ZA^2),
+//     den = 2 Y YA Z^3 w ZA^3,  H = X ZA^2 - XA Z^2 w,  T = Z^2 w ZA^2
+//   (r + n: num - H^2 n T). The signature verifies against the key iff
+//   y_c = num / den is a square root of w with the key's parity — the check
+//   also rejects a compressed key whose x^3 + 7 is not a square (no root
+//   exists), which the y-free parse leaves open. The rare lanes where the
+//   formula does not apply (A or B infinity, A = +-B: H = 0) take an exact
+//   slow path with the square root. hkv_finish_kernel computes the u1 * G sum
+//   (per-window tables: no doublings) and num, num_{r+n}, den;
+//   hkv_yverdict_kernel inverts den by Montgomery's trick over BATCH_INV
+//   signatures per lane and writes the verdict bitmap.
+// ---------------------------------------------------------------------------
+// acc (+inf) += b (+binf), both Jacobian on one curve, exact in every case
+HKV_DEV void gej_add_var(gej& acc, bool& inf, const gej& b, bool binf) {
+  gej a2;
+  fe z2, z3;
+  fe_sqr(z2, b.z);
+  fe_mul(z3, z2, b.z);
+  fe_mul(a2.x, acc.x, z2);
+  fe_mul(a2.y, acc.y, z3);
+  fe_mul(a2.z, acc.z, b.z);
+  bool ainf = inf;
+  gej_accumulate(a2, ainf, acc.z, b.x, b.y, !binf && !inf);
+  const bool take_b = inf && !binf, keep_a = binf;
+  gej_cmov(a2, b, take_b);
+  gej_cmov(a2, acc, keep_a);
+  acc = a2;
+  inf = keep_a ? inf : (take_b ? false : ainf);
+}
+
+// x(R) == r (mod p) for Jacobian (X, ., Z): r Z^2 == X, or (r + n) Z^2 == X when r < p - n
+HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]) {
+  fe zz, X = Xin, t, rf;
+  fe_sqr(zz, Z);
+  fe_normalize(X);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) rf.v[k] = r[k];
+  fe_mul(t, rf, zz);
+  fe_normalize(t);
+  bool eq = fe_eq_norm(t, X);
+  const bool small_r = u256_lt(r, PMN);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) rf.v[k] = addc(r[k], SC_N[k], c);
+  fe_mul(t, rf, zz);
+  fe_normalize(t);
+  return eq || (small_r && fe_eq_norm(t, X));
+}
+
+#ifndef HKV_FINISH_WAVES
+#define HKV_FINISH_WAVES 2  // waves per SIMD the finish kernel's register allocation targets (4: 179 VGPRs
+                            // spilled, 1-2% slower in the same-box A/B)
+#endif
+HKV_DEV void gtab_entry(const uint32_t* __restrict__ gtab, int t, uint32_t gd, fe& tx, fe& ty) {
+  const uint32_t mag = gd & GD_MAG;
+  const uint4* e = reinterpret_cast<const uint4*>(gtab) + ((size_t)t * GTAB_ENTRIES + (mag ? mag - 1 : 0)) * 4;
+  const uint4 a0 = e[0], a1 = e[1], a2 = e[2], a3 = e[3];
+  tx.v[0] = a0.x; tx.v[1] = a0.y; tx.v[2] = a0.z; tx.v[3] = a0.w;
+  tx.v[4] = a1.x; tx.v[5] = a1.y; tx.v[6] = a1.z; tx.v[7] = a1.w;
+  ty.v[0] = a2.x; ty.v[1] = a2.y; ty.v[2] = a2.z; ty.v[3] = a2.w;
+  ty.v[4] = a3.x; ty.v[5] = a3.y; ty.v[6] = a3.z; ty.v[7] = a3.w;
+}
+
+__global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
+                                                        const uint32_t* __restrict__ gtab) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  const bool valid = (i < n) && (flags & FLAG_VALID);
+
+  // ---- A = u1 * G: one affine addition per window, table t = 2j + h holds
+  // multiples of 2^(GTAB_W j + 128 h) G; the next entry is loaded before
+  // the current addition
+  gej A;
+  bool ainf = true;
+  fe_set_zero(A.x);
+  fe_set_zero(A.y);
+  fe_set_zero(A.z);
+  uint32_t gd = valid ? im[(size_t)IM_GDIG * n_pad + i] : 0u;
+  fe tx, ty;
+  gtab_entry(gtab, 0, gd, tx, ty);
+#pragma unroll 1
+  for (int t = 0; t < 2 * GWIN; ++t) {
+    const uint32_t gdn = (t + 1 < 2 * GWIN && valid) ? im[(size_t)(IM_GDIG + t + 1) * n_pad + i] : 0u;
+    fe nx, nyy;
+    if (t + 1 < 2 * GWIN) gtab_entry(gtab, t + 1, gdn, nx, nyy);
+    const bool take = (gd & GD_MAG) != 0;
+    fe nty;
+    fe_neg(nty, ty);
+    fe_cmov(ty, nty, (gd & GD_NEG) != 0);
+    const bool was_inf = ainf;
+    gej_accumulate(A, ainf, A.z, tx, ty, take);
+    if (__any(take && was_inf)) gej_accumulate_from_inf(A, ainf, tx, ty, take && was_inf);
+    gd = gdn;
+    tx = nx;
+    ty = nyy;
+  }
+
+  // ---- B' from the ecmult kernel, w, r (not hoisted above the loop: it
+  // would hold 56 more VGPRs through every addition)
+  asm volatile("" ::: "memory");
+  gej B;
+  fe w;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    B.x.v[k] = im[(size_t)(IM_BX + k) * n_pad + i];
+    B.y.v[k] = im[(size_t)(IM_BX + 8 + k) * n_pad + i];
+    B.z.v[k] = im[(size_t)(IM_BX + 16 + k) * n_pad + i];
+    w.v[k] = im[(size_t)(IM_W + k) * n_pad + i];
+    r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+  }
+  const bool binf = (flags & FLAG_BINF) != 0;
+
+  // ---- num, num_{r+n}, den (formula above), ordered for short live ranges:
+  // a = Y ZA^3, b = YA Z^3 give Y^2 ZA^6 = a^2, YA^2 Z^6 = b^2, den = 2 a b w
+  fe ZA2, ZA3, Z2, Z3, U1, H, T, S1, HH, t, num, numn, den;
+  fe_sqr(ZA2, A.z);
+  fe_mul(ZA3, ZA2, A.z);
+  fe_sqr(Z2, B.z);
+  fe_mul(Z3, Z2, B.z);
+  fe_mul(Z2, Z2, w);            // Z^2 w
+  fe_mul(U1, B.x, ZA2);         // X ZA^2
+  fe_mul(t, A.x, Z2);           // XA Z^2 w
+  fe_sub(H, U1, t);
+  const bool hz = fe_is_zero(H);
+  fe_add(S1, t, U1);
+  fe_mul(T, Z2, ZA2);           // Z^2 w ZA^2
+  {
+    fe rf;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rf.v[k] = r[k];
+    fe_mul(t, rf, T);
+    fe_add(S1, S1, t);          // r T + XA Z^2 w + X ZA^2
+  }
+  fe_sqr(HH, H);
+  fe a, b;
+  fe_mul(a, B.y, ZA3);
+  fe_mul(b, A.y, Z3);
+  fe_mul(den, a, b);
+  fe_mul(den, den, w);
+  fe_add(den, den, den);        // 2 Y YA Z^3 w ZA^3
+  fe_sqr(num, a);               // Y^2 ZA^6
+  fe_sqr(t, w);
+  fe_mul(t, t, w);              // w^3
+  fe_sqr(b, b);                 // YA^2 Z^6
+  fe_mul(t, t, b);
+  fe_add(num, num, t);
+  fe_mul(t, HH, S1);
+  fe_sub(num, num, t);
+  {
+    fe nf;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nf.v[k] = SC_N[k];
+    fe_mul(t, T, nf);
+    fe_mul(t, HH, t);
+    fe_sub(numn, num, t);       // the r + n candidate
+  }
+
+  uint32_t fo = flags;
+  if (!valid) fo |= FLAG_DECIDED;
+  // the formula needs A, B finite and A != +-B; those lanes (adversarial
+  // only: u1 = 0, or u1 G = +-u2 Q) keep B' and park A for hkv_rare_kernel
+  const bool rare = valid && (ainf || binf || hz);
+  if (rare) {
+    fo |= FLAG_RARE | (ainf ? FLAG_AINF : 0u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      im[(size_t)(IM_AX + k) * n_pad + i] = A.x.v[k];
+      im[(size_t)(IM_AY + k) * n_pad + i] = A.y.v[k];
+      im[(size_t)(IM_AY + 8 + k) * n_pad + i] = A.z.v[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      im[(size_t)(IM_NUM + k) * n_pad + i] = num.v[k];
+      im[(size_t)(IM_NUM + 8 + k) * n_pad + i] = numn.v[k];
+      im[(size_t)(IM_DEN + k) * n_pad + i] = den.v[k];
+    }
+  }
+  im[(size_t)IM_FLAGS * n_pad + i] = fo;
+}
+
+// the exact slow path for the finish kernel's rare lanes: y0 = sqrt(w) of
+// the key's parity (no root: the key does not parse), B on E = (X, Y, Z y0)
+// (phi^-1 of B'), R = A + B with every degenerate case, the x compare.
+// A wave without a rare lane returns after one flags load.
+__global__ void __launch_bounds__(WG) hkv_rare_kernel(uint32_t* __restrict__ im, uint32_t n_pad) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  const bool rare = (flags & FLAG_RARE) != 0;
+  if (!__any(rare)) return;
+  gej A, B;
+  fe w;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A.x.v[k] = im[(size_t)(IM_AX + k) * n_pad + i];
+    A.y.v[k] = im[(size_t)(IM_AY + k) * n_pad + i];
+    A.z.v[k] = im[(size_t)(IM_AY + 8 + k) * n_pad + i];
+    B.x.v[k] = im[(size_t)(IM_BX + k) * n_pad + i];
+    B.y.v[k] = im[(size_t)(IM_BX + 8 + k) * n_pad + i];
+    B.z.v[k] = im[(size_t)(IM_BX + 16 + k) * n_pad + i];
+    w.v[k] = im[(size_t)(IM_W + k) * n_pad + i];
+    r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+  }
+  fe y0, y2, ny;
+  fe_sqrt_cand(y0, w);
+  fe_sqr(y2, y0);
+  const bool is_sq = fe_equal(y2, w);
+  fe_normalize(y0);
+  fe_neg(ny, y0);
+  fe_normalize(ny);
+  if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
+  gej b = B;
+  fe_mul(b.z, B.z, y0);
+  bool rinf = (flags & FLAG_AINF) != 0;
+  gej_add_var(A, rinf, b, (flags & FLAG_BINF) != 0);
+  const bool acc_ok = is_sq && !rinf && x_matches_r(A.x, A.z, r);
+  if (rare) im[(size_t)IM_FLAGS * n_pad + i] = flags | FLAG_DECIDED | (acc_ok ? FLAG_ACCEPT : 0u);
+}
+
+// verdicts: den^-1 by Montgomery's trick over BATCH_INV signatures per lane
+// (signature i = t + k * stride; stride % WG == 0, so a wave's 64 lanes hold
+// 64 consecutive signatures and their verdicts leave as one ballot word)
+__global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t stride,
+                                                          uint32_t* __restrict__ bits, uint32_t n_words) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  fe c;
+  fe_set_u32(c, 1);
+#pragma unroll 1
+  for (int k = 0; k < BATCH_INV; ++k) {
+    const uint32_t i = t + (uint32_t)k * stride;
+    if (i >= n_pad) break;
+    const bool decided = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_DECIDED) != 0;
+    fe d;
+    im_load8(im, n_pad, IM_DEN, i, d.v);
+    if (decided) fe_set_u32(d, 1);
+    fe_mul(c, c, d);
+    im_store8(im, n_pad, IM_C, i, c.v);
+  }
+  fe inv;
+  fe_inv(inv, c);
+#pragma unroll 1
+  for (int k = BATCH_INV - 1; k >= 0; --k) {
+    const uint32_t i = t + (uint32_t)k * stride;
+    if (i >= n_pad) continue;  // wave-uniform: n_pad and stride are multiples of 64
+    const uint32_t f = im[(size_t)IM_FLAGS * n_pad + i];
+    const bool decided = (f & FLAG_DECIDED) != 0;
+    fe prev, dinv, d;
+    if (k > 0) {
+      im_load8(im, n_pad, IM_C, i - stride, prev.v);
+    } else {
+      fe_set_u32(prev, 1);
+    }
+    fe_mul(dinv, inv, prev);
+    im_load8(im, n_pad, IM_DEN, i, d.v);
+    if (decided) fe_set_u32(d, 1);
+    fe_mul(inv, inv, d);
+    bool accept = (f & FLAG_ACCEPT) != 0;
+    if (!decided) {
+      fe num, w, yc, y2;
+      uint32_t r[8];
+      im_load8(im, n_pad, IM_NUM, i, num.v);
+      im_load8(im, n_pad, IM_W, i, w.v);
+      im_load8(im, n_pad, IM_R, i, r);
+      const uint32_t want = (f & FLAG_YODD) ? 1u : 0u;
+      fe_mul(yc, num, dinv);
+      fe_normalize(yc);
+      fe_sqr(y2, yc);
+      bool ok = fe_equal(y2, w) && (yc.v[0] & 1u) == want;
+      const bool small_r = u256_lt(r, PMN);
+      if (__any(!ok && small_r)) {
+        im_load8(im, n_pad, IM_NUM + 8, i, num.v);
+        fe_mul(yc, num, dinv);
+        fe_normalize(yc);
+        fe_sqr(y2, yc);
+        ok = ok || (small_r && fe_equal(y2, w) && (yc.v[0] & 1u) == want);
+      }
+      accept = ok;
+    }
+    const uint64_t ball = __ballot(accept);
+    if ((threadIdx.x & 63) == 0) {
+      const uint32_t wi = i / 32;
+      if (wi < n_words) bits[wi] = (uint32_t)ball;
+      if (wi + 1 < n_words) bits[wi + 1] = (uint32_t)(ball >> 32);
+    }
+  }
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // shared helpers for table init / generators: simple MSB-first double-and-add
@@ -787,16 +1148,26 @@ HKV_DEV bool ecmult_simple(ge& out, const sc& a, const sc& b, const ge& p) {
   return true;
 }
 
-// 3. fixed-base tables: entry j (1..128) of table t = j * (2^(128 t) G)
+// 3. fixed-base tables: entry j (1..2^(GTAB_W-1)) of table t = 2 w + h is
+//    j * 2^(GTAB_W w + 128 h) G (mod n): tables 0 and 1 are j * G and
+//    j * 2^128 G; the y-free finish kernel uses all GTAB_TABLES.
 __global__ void __launch_bounds__(WG) hkv_gtable_kernel(uint32_t* __restrict__ gtab) {
   const int tid = blockIdx.x * WG + threadIdx.x;
-  if (tid >= 2 * GTAB_ENTRIES) return;
+  if (tid >= GTAB_TABLES * GTAB_ENTRIES) return;
   const int t = tid / GTAB_ENTRIES, j = tid % GTAB_ENTRIES + 1;
   sc a, zero;
 #pragma unroll
   for (int k = 0; k < 8; ++k) { a.v[k] = 0; zero.v[k] = 0; }
-  // scalar j * 2^(128 t)
-  a.v[t * 4] = (uint32_t)j;
+  // scalar j * 2^(GTAB_W (t / 2) + 128 (t % 2)) mod n: 2^off (off < 256, < n) times j
+  {
+    const int off = GTAB_W * (t / 2) + 128 * (t % 2);
+    sc p2, jj;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { p2.v[k] = 0; jj.v[k] = 0; }
+    p2.v[off >> 5] = 1u << (off & 31);
+    jj.v[0] = (uint32_t)j;
+    sc_mul(a, jj, p2);
+  }
   ge g, out;
   ge_set_g(g);
   ecmult_simple(out, a, zero, g);
@@ -1061,7 +1432,7 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
-hipError_t launch_ecmult(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
+hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, unsigned long long* clk,
                          hipStream_t st) {
   if (split)
@@ -1078,8 +1449,27 @@ hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hip
   return hipGetLastError();
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div(2 * GTAB_ENTRIES, WG)), dim3(WG), 0, st, gtab);
+  hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div((size_t)GTAB_TABLES * GTAB_ENTRIES, WG)), dim3(WG), 0, st,
+                     gtab);
   return hipGetLastError();
+}
+hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* bits,
+                         uint32_t n_words, hipStream_t st) {
+#if HKV_YFREE
+  hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // BATCH_INV signatures per lane, the stride a multiple of WG (n_pad is)
+  const uint32_t stride = ceil_div(ceil_div(n_pad, BATCH_INV), WG) * WG;
+  hipLaunchKernelGGL(hkv_yverdict_kernel, dim3(stride / WG), dim3(WG), 0, st, im, n_pad, stride, bits, n_words);
+  return hipGetLastError();
+#else
+  (void)im; (void)n; (void)n_pad; (void)gtab; (void)bits; (void)n_words; (void)st;
+  return hipSuccess;
+#endif
 }
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st) {
   hipLaunchKernelGGL(hkv_gen_pool_kernel, dim3(ceil_div(npool, WG)), dim3(WG), 0, st, seed, npool, pool);

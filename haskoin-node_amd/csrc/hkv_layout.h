@@ -61,12 +61,42 @@ constexpr uint32_t DIG_ZERO = (uint32_t)QBIAS | ((uint32_t)QBIAS << QDIG_BITS);
 constexpr int BATCH_INV = 16;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
-// Fixed-base tables in HBM (64 MiB, MALL resident): multiples j*B for
-// j = 1..2^19, B in {G, 2^128 G}, affine, 16 dwords per entry
-// [x(8) | y(8)], table t at entry offset t*2^19. Gathered per lane by
-// LDS-DMA at the start of the window that adds them (four doublings ahead).
+// y-free verification (HKV_YFREE, full-grid batches; hkv_kernels.hip §2b):
+// the prologue stores w = x^3 + 7 over IM_QY instead of solving y = sqrt(w);
+// ecmult runs u2 * Q' on E_w : y^2 = x^3 + 7 w^3 with Q' = (x w, w^2) and
+// leaves B' = (X, Y, Z) over the Q-digit words; the finish kernel adds the
+// u1 * G sum from per-window tables and reduces "x(u1 G + u2 Q) == r" to
+// y_c = num / den, accepted iff y_c^2 == w with the key's y parity.
+#ifndef HKV_YFREE
+#define HKV_YFREE 1
+#endif
+constexpr uint32_t FLAG_YODD = 16u;      // the key's y is odd (prefix 03/07, or the 04 key's y)
+constexpr uint32_t FLAG_COMP = 32u;      // compressed key: x^3 + 7 not yet shown to be a square
+constexpr uint32_t FLAG_BINF = 64u;      // B' = u2 * Q' is infinity
+constexpr uint32_t FLAG_DECIDED = 128u;  // the finish kernel decided the verdict (rare cases)
+constexpr uint32_t FLAG_ACCEPT = 256u;   // ... and it is accept
+constexpr uint32_t FLAG_RARE = 512u;     // A or B infinity, or A = +-B: the exact slow path decides
+constexpr uint32_t FLAG_AINF = 1024u;    // A = u1 * G is infinity (u1 = 0)
+enum : int {
+  IM_W = IM_QY,         // 8 limbs, w = x^3 + 7 (normalised)
+  IM_BX = IM_DIG,       // 3 x 8 limbs: B' = (X, Y, Z) Jacobian on E_w (ecmult -> finish)
+  IM_NUM = IM_DIG,      // 3 x 8 limbs: num_r, num_{r+n}, den (finish -> verdict kernel)
+  IM_DEN = IM_DIG + 16,
+  IM_AX = IM_QX,        // rare lanes: A = u1 * G parked over x (8) and K1..U1H (16)
+  IM_AY = IM_K1,
+};
+static_assert(IM_AY + 16 <= IM_R, "A fits below r");
+static_assert(IM_DIG + 24 <= IM_GDIG, "B' and num/den fit over the Q digits");
+
+// Fixed-base tables in HBM: multiples j*B for j = 1..2^19, affine, 16 dwords
+// per entry [x(8) | y(8)], table t at entry offset t*2^19. Tables 0 and 1
+// (64 MiB, MALL resident) are B = G and 2^128 G: the split ecmult gathers
+// them per lane by LDS-DMA at the start of the window that adds them (four
+// doublings ahead). With HKV_YFREE, tables 2j + h (j = 1..GWIN-1) hold
+// B = 2^(GTAB_W j + 128 h) G, so the finish kernel sums u1 * G without doublings.
 constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
-constexpr size_t GTAB_DWORDS = 2ull * GTAB_ENTRIES * 16;
+constexpr int GTAB_TABLES = HKV_YFREE ? 2 * GWIN : 2;
+constexpr size_t GTAB_DWORDS = (size_t)GTAB_TABLES * GTAB_ENTRIES * 16;
 
 // Per-lane Q table: multiples j*Q, j = 1..QBIAS, affine on the lane's isomorphic
 // curve; per entry 6 quads (16 B): x(2) | y(2) | beta*x(2); entry e of lane L

@@ -9,10 +9,12 @@ measured ``v_mad_u64_u32`` issue rate (profiles/r01_ubench_int.json:
 """
 from __future__ import annotations
 
-# limb products per primitive
-MUL256 = 64          # 8x8 schoolbook rows
-SQR256 = 28 + 8      # off-diagonal + diagonal
-FE_RED = 8 + 1       # H*977 chain + top fold (y = top*977)
+# limb products per primitive (hkv_mul_asm.h, HKV_MUL_RED: the reduction
+# folded into the scan; the 7 carry-in mads by 1 per product are not limb
+# products and are not counted)
+MUL256 = 64          # 8x8 column scan
+SQR256 = 43          # 8 squares + 7 a_i * 2a_{i+1} + 28 a_i * (2a)_j (incl. the 1-bit top limb)
+FE_RED = 8 + 1       # h_j * 977 in the low columns + top fold (y = top*977)
 FE_MUL = MUL256 + FE_RED
 FE_SQR = SQR256 + FE_RED
 FE_MUL_SMALL = 8 + 1
@@ -34,7 +36,12 @@ SC_INV_LOW = 0x0BAAEDCE6AF48A03BBFD25E8CD036413F
 BATCH_INV = 16       # signatures per s^-1 (hkv_layout.h)
 
 
+YFREE = True         # full-grid batches verify y-free (hkv_layout.h HKV_YFREE)
+
+
 def ecmult_products() -> int:
+    """The ecmult stage: hkv_ecmult_kernel, plus (y-free) the finish and
+    verdict kernels that complete u1*G + u2*Q and decide x(R) == r."""
     table = (GEJ_DOUBLE                      # 2Q
              + FE_SQR + 3 * FE_MUL           # Q' = (x Z^2, y Z^3)
              + (Q_TABLE - 2) * GEJ_ADD_GE    # 3Q .. Q_TABLE*Q
@@ -42,14 +49,22 @@ def ecmult_products() -> int:
              + FE_MUL                        # beta * x of the last entry
              + (Q_TABLE - 2) * (5 * FE_MUL + FE_SQR)   # rescale entries 2..Q_TABLE-1 (+ rho step, beta)
              + (4 * FE_MUL + FE_SQR))        # rescale entry 1
-    ladder = DOUBLINGS * GEJ_DOUBLE + 2 * Q_WINDOWS * GEJ_ADD_GE + 2 * G_WINDOWS * GEJ_ADD_ZINV
-    compare = 3 * FE_MUL + FE_SQR
-    return table + ladder + compare
+    if not YFREE:
+        ladder = DOUBLINGS * GEJ_DOUBLE + 2 * Q_WINDOWS * GEJ_ADD_GE + 2 * G_WINDOWS * GEJ_ADD_ZINV
+        compare = 3 * FE_MUL + FE_SQR
+        return table + ladder + compare
+    to_ew = FE_MUL + FE_SQR                              # Q' = (x w, w^2) on E_w
+    ladder = DOUBLINGS * GEJ_DOUBLE + 2 * Q_WINDOWS * GEJ_ADD_GE + FE_MUL   # + Z = acc.z * Zg
+    g_sum = (2 * G_WINDOWS - 1) * GEJ_ADD_GE             # per-window tables, no doublings
+    combine = 16 * FE_MUL + 6 * FE_SQR                   # num, num_{r+n}, den (hkv_finish_kernel)
+    inv_chain = 255 * FE_SQR + 15 * FE_MUL               # fe_inv, one per BATCH_INV signatures
+    verdict = 3 * FE_MUL + inv_chain // BATCH_INV + FE_MUL + FE_SQR   # y_c = num / den, y_c^2 == w
+    return table + to_ew + ladder + g_sum + combine + verdict
 
 
 def prologue_products() -> int:
     chain223 = 222 * FE_SQR + 11 * FE_MUL
-    sqrt = chain223 + (23 + 6 + 2) * FE_SQR + 2 * FE_MUL
+    sqrt = 0 if YFREE else chain223 + (23 + 6 + 2) * FE_SQR + 2 * FE_MUL
     curve = FE_SQR + FE_MUL + FE_SQR                 # x^3 + 7, y^2 check
     x127 = (1 + 1 + 3 + 6 + 12 + 24 + 48 + 24 + 6 + 1) * SC_SQR + 10 * SC_MUL
     inv = x127 + 129 * SC_SQR + bin(SC_INV_LOW).count("1") * SC_MUL
@@ -69,20 +84,25 @@ def prologue_products() -> int:
 # 2^128 G by precomputed w = 15 tables (ECMULT_WINDOW_SIZE default) added with
 # secp256k1_gej_add_zinv_var, 129 doublings (secp256k1_gej_double: 3M + 4S),
 # then the Jacobian x compare (1S + 1M). Field products are priced at this
-# ISA's 32-bit limb-product counts (FE_MUL / FE_SQR above).
+# ISA's 32-bit limb-product counts as they stood when the numerator was
+# frozen (round 1: 64 + 9 per multiply, 36 + 9 per square), not at the
+# current kernels' counts above.
+REF_FE_MUL = 64 + 9
+REF_FE_SQR = 36 + 9
 REF_BITS = 129                      # |k1|, |k2| < 2^129 after the GLV split
 REF_WNAF_Q = 5
 REF_WINDOW_G = 15
 REF_Q_ADDS = 2 * REF_BITS / (REF_WNAF_Q + 1)     # 43
 REF_G_ADDS = 2 * 128 / (REF_WINDOW_G + 1)        # 16
-REF_TABLE = ((3 * FE_MUL + 4 * FE_SQR)            # 2Q
-             + 7 * (8 * FE_MUL + 3 * FE_SQR)      # 3Q .. 15Q (odd multiples, mixed adds)
-             + 7 * (4 * FE_MUL + FE_SQR)          # global-Z rescale
-             + 8 * FE_MUL)                        # lambda table: beta * x
-REF_LADDER = (REF_BITS * (3 * FE_MUL + 4 * FE_SQR) + REF_Q_ADDS * (8 * FE_MUL + 3 * FE_SQR)
-              + REF_G_ADDS * (9 * FE_MUL + 3 * FE_SQR))
-REF_COMPARE = FE_SQR + FE_MUL
+REF_TABLE = ((3 * REF_FE_MUL + 4 * REF_FE_SQR)            # 2Q
+             + 7 * (8 * REF_FE_MUL + 3 * REF_FE_SQR)      # 3Q .. 15Q (odd multiples, mixed adds)
+             + 7 * (4 * REF_FE_MUL + REF_FE_SQR)          # global-Z rescale
+             + 8 * REF_FE_MUL)                            # lambda table: beta * x
+REF_LADDER = (REF_BITS * (3 * REF_FE_MUL + 4 * REF_FE_SQR) + REF_Q_ADDS * (8 * REF_FE_MUL + 3 * REF_FE_SQR)
+              + REF_G_ADDS * (9 * REF_FE_MUL + 3 * REF_FE_SQR))
+REF_COMPARE = REF_FE_SQR + REF_FE_MUL
 P_ALG_ECMULT = int(round(REF_TABLE + REF_LADDER + REF_COMPARE))
+assert P_ALG_ECMULT == 103553, "the frozen numerator must not drift"
 
 ECMULT_PRODUCTS_PER_VERIFY = ecmult_products()
 PROLOGUE_PRODUCTS_PER_VERIFY = prologue_products()
