@@ -58,6 +58,7 @@ struct DevCtx {
   uint64_t ms_seq = 0;           // last sequence number handed to hkv_ms_scan_kernel
   uint64_t* ms_total_dev = nullptr;  // its device-side address
   void* ms_ctr = nullptr;            // device counters of hkv_ms_scan_kernel
+  uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -166,7 +167,7 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
           "ecmult launch");
   // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
   // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)
-  if (!split && HKV_YFREE) HKV_TRY(hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, vbits, n_words, st),
+  if (!split && HKV_YFREE) HKV_TRY(hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st),
                                    "finish launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
@@ -198,6 +199,8 @@ int init_device(DevCtx& d, int device) {
   // total + finished-workgroup count; the scan kernel re-arms them itself
   HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
+  HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
+  HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
   HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
@@ -237,6 +240,7 @@ void free_device(DevCtx& d) {
     if (p) (void)hipFree(p);
   if (d.ms_total) (void)hipHostFree(d.ms_total);
   if (d.ms_ctr) (void)hipFree(d.ms_ctr);
+  if (d.rare_ctr) (void)hipFree(d.rare_ctr);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.clk) (void)hipFree(d.clk);
   if (d.last_use) (void)hipEventDestroy(d.last_use);

@@ -32,8 +32,8 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 // y-free full-grid batches (HKV_YFREE): u1 * G, the y0 = num / den reduction and the verdict bitmap
-hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* bits,
-                         uint32_t n_words, hipStream_t st);
+hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
+                         uint32_t* bits, uint32_t n_words, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
 hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,
                               uint32_t unc_permille, void* recs, hipStream_t st);

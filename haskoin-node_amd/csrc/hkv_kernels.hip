@@ -864,6 +864,12 @@ HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]) {
   return eq || (small_r && fe_eq_norm(t, X));
 }
 
+// signatures per lane of the verdict kernel: one Fermat den^-1 (255S + 15M,
+// a dependent chain) per lane, 3 multiplications per signature
+#ifndef HKV_VERDICT_BATCH
+#define HKV_VERDICT_BATCH 16
+#endif
+constexpr int VERDICT_BATCH = HKV_VERDICT_BATCH;
 #ifndef HKV_FINISH_WAVES
 #define HKV_FINISH_WAVES 2  // waves per SIMD the finish kernel's register allocation targets (4: 179 VGPRs
                             // spilled, 1-2% slower in the same-box A/B)
@@ -879,7 +885,8 @@ HKV_DEV void gtab_entry(const uint32_t* __restrict__ gtab, int t, uint32_t gd, f
 }
 
 __global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
-                                                        const uint32_t* __restrict__ gtab) {
+                                                        const uint32_t* __restrict__ gtab,
+                                                        uint32_t* __restrict__ rare_ctr) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n_pad) return;
   const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
@@ -979,6 +986,19 @@ __global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32
   // the formula needs A, B finite and A != +-B; those lanes (adversarial
   // only: u1 = 0, or u1 G = +-u2 Q) keep B' and park A for hkv_rare_kernel
   const bool rare = valid && (ainf || binf || hz);
+  // compact the rare lanes' indices (one atomic per wave) so the slow path
+  // runs in dense waves: in an adversarial batch ~1-2% of the lanes are rare,
+  // which would put one in most waves
+  const uint64_t rmask = __ballot(rare);
+  if (rmask) {
+    uint32_t base = 0;
+    const int lead = __builtin_ctzll(rmask);
+    if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(rare_ctr, (uint32_t)__popcll(rmask));
+    base = __shfl(base, lead);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rmask >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)rmask, 0u));
+    if (rare) im[(size_t)IM_RARE_LIST * n_pad + base + rank] = i;
+  }
   if (rare) {
     fo |= FLAG_RARE | (ainf ? FLAG_AINF : 0u);
 #pragma unroll
@@ -1001,13 +1021,14 @@ __global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32
 // the exact slow path for the finish kernel's rare lanes: y0 = sqrt(w) of
 // the key's parity (no root: the key does not parse), B on E = (X, Y, Z y0)
 // (phi^-1 of B'), R = A + B with every degenerate case, the x compare.
-// A wave without a rare lane returns after one flags load.
-__global__ void __launch_bounds__(WG) hkv_rare_kernel(uint32_t* __restrict__ im, uint32_t n_pad) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n_pad) return;
+// Lane k takes the k-th compacted rare index; lanes past the count return.
+__global__ void __launch_bounds__(WG) hkv_rare_kernel(uint32_t* __restrict__ im, uint32_t n_pad,
+                                                      const uint32_t* __restrict__ rare_ctr) {
+  const uint32_t k = blockIdx.x * WG + threadIdx.x;
+  if (k >= *rare_ctr) return;
+  const uint32_t i = im[(size_t)IM_RARE_LIST * n_pad + k];
   const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-  const bool rare = (flags & FLAG_RARE) != 0;
-  if (!__any(rare)) return;
+  const bool rare = true;
   gej A, B;
   fe w;
   uint32_t r[8];
@@ -1038,16 +1059,18 @@ __global__ void __launch_bounds__(WG) hkv_rare_kernel(uint32_t* __restrict__ im,
   if (rare) im[(size_t)IM_FLAGS * n_pad + i] = flags | FLAG_DECIDED | (acc_ok ? FLAG_ACCEPT : 0u);
 }
 
-// verdicts: den^-1 by Montgomery's trick over BATCH_INV signatures per lane
+// verdicts: den^-1 by Montgomery's trick over VERDICT_BATCH signatures per lane
 // (signature i = t + k * stride; stride % WG == 0, so a wave's 64 lanes hold
 // 64 consecutive signatures and their verdicts leave as one ballot word)
 __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t stride,
-                                                          uint32_t* __restrict__ bits, uint32_t n_words) {
+                                                          uint32_t* __restrict__ bits, uint32_t n_words,
+                                                          uint32_t* __restrict__ rare_ctr) {
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t == 0) *rare_ctr = 0;  // re-arm for the next batch (the rare kernel has read it)
   fe c;
   fe_set_u32(c, 1);
 #pragma unroll 1
-  for (int k = 0; k < BATCH_INV; ++k) {
+  for (int k = 0; k < VERDICT_BATCH; ++k) {
     const uint32_t i = t + (uint32_t)k * stride;
     if (i >= n_pad) break;
     const bool decided = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_DECIDED) != 0;
@@ -1060,7 +1083,7 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
   fe inv;
   fe_inv(inv, c);
 #pragma unroll 1
-  for (int k = BATCH_INV - 1; k >= 0; --k) {
+  for (int k = VERDICT_BATCH - 1; k >= 0; --k) {
     const uint32_t i = t + (uint32_t)k * stride;
     if (i >= n_pad) continue;  // wave-uniform: n_pad and stride are multiples of 64
     const uint32_t f = im[(size_t)IM_FLAGS * n_pad + i];
@@ -1453,21 +1476,22 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
                      gtab);
   return hipGetLastError();
 }
-hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* bits,
-                         uint32_t n_words, hipStream_t st) {
+hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
+                         uint32_t* bits, uint32_t n_words, hipStream_t st) {
 #if HKV_YFREE
-  hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab);
+  hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, rare_ctr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad);
+  hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad, (const uint32_t*)rare_ctr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // BATCH_INV signatures per lane, the stride a multiple of WG (n_pad is)
-  const uint32_t stride = ceil_div(ceil_div(n_pad, BATCH_INV), WG) * WG;
-  hipLaunchKernelGGL(hkv_yverdict_kernel, dim3(stride / WG), dim3(WG), 0, st, im, n_pad, stride, bits, n_words);
+  // VERDICT_BATCH signatures per lane, the stride a multiple of WG (n_pad is)
+  const uint32_t stride = ceil_div(ceil_div(n_pad, VERDICT_BATCH), WG) * WG;
+  hipLaunchKernelGGL(hkv_yverdict_kernel, dim3(stride / WG), dim3(WG), 0, st, im, n_pad, stride, bits, n_words,
+                     rare_ctr);
   return hipGetLastError();
 #else
-  (void)im; (void)n; (void)n_pad; (void)gtab; (void)bits; (void)n_words; (void)st;
+  (void)im; (void)n; (void)n_pad; (void)gtab; (void)rare_ctr; (void)bits; (void)n_words; (void)st;
   return hipSuccess;
 #endif
 }

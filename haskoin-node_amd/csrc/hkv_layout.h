@@ -85,7 +85,8 @@ enum : int {
   IM_AX = IM_QX,        // rare lanes: A = u1 * G parked over x (8) and K1..U1H (16)
   IM_AY = IM_K1,
 };
-static_assert(IM_AY + 16 <= IM_R, "A fits below r");
+constexpr int IM_RARE_LIST = IM_AY + 16;  // the finish kernel's compacted rare-lane indices
+static_assert(IM_RARE_LIST < IM_R, "A and the rare list fit below r");
 static_assert(IM_DIG + 24 <= IM_GDIG, "B' and num/den fit over the Q digits");
 
 // Fixed-base tables in HBM: multiples j*B for j = 1..2^19, affine, 16 dwords
