@@ -163,7 +163,7 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split,
-                             d.profile ? d.clk : nullptr, st),
+                             d.profile ? d.clk : nullptr, d.rare_ctr, st),
           "ecmult launch");
   // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
   // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)

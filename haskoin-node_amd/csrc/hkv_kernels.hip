@@ -486,12 +486,24 @@ HKV_DEV void ec_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, cons
   else gej_accumulate(acc, inf, az, tx, ty, take);
 }
 
+#if HKV_YFREE
+HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
+                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags);
+#endif
+// HKV_FUSE_FINISH: the full-grid ecmult kernel runs the finish (u1 * G, num,
+// den) itself after storing B', at its own occupancy, instead of a separate
+// hkv_finish_kernel launch. Measured 1-2% slower (the fused kernel spills 168
+// VGPRs at 4 waves per SIMD; profiles/r02_variants_fuse.log), so off.
+#ifndef HKV_FUSE_FINISH
+#define HKV_FUSE_FINISH 0
+#endif
 template <bool SPLIT>
 __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits, uint32_t n_words,
-                                                        unsigned long long* __restrict__ clk) {
+                                                        unsigned long long* __restrict__ clk,
+                                                        uint32_t* __restrict__ rare_ctr) {
   // per wave: two G-entry slots (one in SPLIT mode: a wave adds one G term),
   // each 4 quads x 64 lanes x 16 B (LDS-DMA target); in SPLIT mode reused
   // after the window loop for the half-sum exchange
@@ -763,6 +775,9 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
         im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
       }
       im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
+#if HKV_FUSE_FINISH
+      finish_lane(im, n, n_pad, gtab, rare_ctr, i, flags | (inf ? FLAG_BINF : 0u));
+#endif
       continue;
     }
 #endif
@@ -884,12 +899,11 @@ HKV_DEV void gtab_entry(const uint32_t* __restrict__ gtab, int t, uint32_t gd, f
   ty.v[4] = a3.x; ty.v[5] = a3.y; ty.v[6] = a3.z; ty.v[7] = a3.w;
 }
 
-__global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
-                                                        const uint32_t* __restrict__ gtab,
-                                                        uint32_t* __restrict__ rare_ctr) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n_pad) return;
-  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+// one signature's finish (hkv_finish_kernel, or the ecmult kernel's own
+// tail with HKV_FUSE_FINISH): whole waves call it (the rare-lane compaction
+// ballots)
+HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
+                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags) {
   const bool valid = (i < n) && (flags & FLAG_VALID);
 
   // ---- A = u1 * G: one affine addition per window, table t = 2j + h holds
@@ -1016,6 +1030,14 @@ __global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32
     }
   }
   im[(size_t)IM_FLAGS * n_pad + i] = fo;
+}
+
+__global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
+                                                        const uint32_t* __restrict__ gtab,
+                                                        uint32_t* __restrict__ rare_ctr) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  finish_lane(im, n, n_pad, gtab, rare_ctr, i, im[(size_t)IM_FLAGS * n_pad + i]);
 }
 
 // the exact slow path for the finish kernel's rare lanes: y0 = sqrt(w) of
@@ -1457,13 +1479,13 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
 }
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, unsigned long long* clk,
-                         hipStream_t st) {
+                         uint32_t* rare_ctr, hipStream_t st) {
   if (split)
     hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, n_words,
-                       clk);
+                       clk, rare_ctr);
   else
     hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, n_words,
-                       clk);
+                       clk, rare_ctr);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {
@@ -1479,9 +1501,12 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st) {
 #if HKV_YFREE
-  hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, rare_ctr);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (!HKV_FUSE_FINISH) {
+    hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, rare_ctr);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad, (const uint32_t*)rare_ctr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
