@@ -408,6 +408,10 @@ __global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* 
   }
 }
 
+// table-entry sign: fe_cneg (XOR + 2-limb fix-up) instead of fe_neg + selects
+#ifndef HKV_CNEG
+#define HKV_CNEG 1
+#endif
 // ---------------------------------------------------------------------------
 // 2. ecmult + x compare
 // ---------------------------------------------------------------------------
@@ -672,9 +676,13 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
           qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
           qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
         }
+#if HKV_CNEG
+        fe_cneg(ty, ty, neg);
+#else
         fe nty;
         fe_neg(nty, ty);
         fe_cmov(ty, nty, neg);
+#endif
         const bool was_inf = inf;
         ec_accumulate<SPLIT && HKV_SPLIT_ILP>(acc, inf, acc.z, tx, ty, take);
         // only the first nonzero digit of a lane starts from infinity: skip
@@ -699,9 +707,13 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
             ty.v[0] = a2.x; ty.v[1] = a2.y; ty.v[2] = a2.z; ty.v[3] = a2.w;
             ty.v[4] = a3.x; ty.v[5] = a3.y; ty.v[6] = a3.z; ty.v[7] = a3.w;
           }
+#if HKV_CNEG
+          fe_cneg(ty, ty, (gd & GD_NEG) != 0);
+#else
           fe nty;
           fe_neg(nty, ty);
           fe_cmov(ty, nty, (gd & GD_NEG) != 0);
+#endif
           fe az;
           fe_mul(az, acc.z, Zg);
           const bool was_inf = inf;
@@ -885,6 +897,11 @@ HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]) {
 #define HKV_VERDICT_BATCH 16
 #endif
 constexpr int VERDICT_BATCH = HKV_VERDICT_BATCH;
+// den^-1: Bernstein-Yang safegcd mod p (hkv_safegcd.h, 750 divsteps) instead of
+// the Fermat chain (255S + 15M)
+#ifndef HKV_VERDICT_SAFEGCD
+#define HKV_VERDICT_SAFEGCD 1
+#endif
 #ifndef HKV_FINISH_WAVES
 #define HKV_FINISH_WAVES 2  // waves per SIMD the finish kernel's register allocation targets (4: 179 VGPRs
                             // spilled, 1-2% slower in the same-box A/B)
@@ -923,9 +940,13 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
     fe nx, nyy;
     if (t + 1 < 2 * GWIN) gtab_entry(gtab, t + 1, gdn, nx, nyy);
     const bool take = (gd & GD_MAG) != 0;
+#if HKV_CNEG
+    fe_cneg(ty, ty, (gd & GD_NEG) != 0);
+#else
     fe nty;
     fe_neg(nty, ty);
     fe_cmov(ty, nty, (gd & GD_NEG) != 0);
+#endif
     const bool was_inf = ainf;
     gej_accumulate(A, ainf, A.z, tx, ty, take);
     if (__any(take && was_inf)) gej_accumulate_from_inf(A, ainf, tx, ty, take && was_inf);
@@ -1103,7 +1124,12 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
     im_store8(im, n_pad, IM_C, i, c.v);
   }
   fe inv;
+#if HKV_VERDICT_SAFEGCD
+  fe_normalize(c);  // safegcd wants 0 < c < p
+  sgcd::inv_mod_p(inv.v, c.v);
+#else
   fe_inv(inv, c);
+#endif
 #pragma unroll 1
   for (int k = VERDICT_BATCH - 1; k >= 0; --k) {
     const uint32_t i = t + (uint32_t)k * stride;

@@ -18,6 +18,12 @@
 //
 // Written __host__ __device__ so the host build (tests/test_safegcd.py)
 // checks the same code the kernels run.
+//
+// Attribution: the signed-30 divstep / matrix-update structure (in
+// particular update_de's sign masks and the "md -= (m^-1 * cd + md) mod 2^30"
+// correction that makes the division by 2^30 exact) follows libsecp256k1's
+// src/modinv32_impl.h (MIT License, Copyright (c) 2020 Peter Dettman and the
+// libsecp256k1 contributors), itself an implementation of the paper above.
 #pragma once
 #include <stdint.h>
 
@@ -31,10 +37,18 @@ namespace hkv {
 namespace sgcd {
 
 constexpr uint32_t M30 = 0x3FFFFFFFu;
-// n in signed30 limbs, and n^-1 mod 2^30
-constexpr int32_t NL[9] = {0x10364141, 0x3F497A33, 0x348A03BB, 0x2BB739AB, 0x3FFFFEBA,
-                           0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0xFFFF};
-constexpr uint32_t NINV30 = 0x2A774EC1u;
+// moduli in signed30 limbs with their inverse mod 2^30: the group order n
+// (s^-1 in hkv_inv_kernel) and the field prime p (den^-1 in hkv_yverdict_kernel)
+struct ModN {
+  static constexpr int32_t L[9] = {0x10364141, 0x3F497A33, 0x348A03BB, 0x2BB739AB, 0x3FFFFEBA,
+                                   0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0xFFFF};
+  static constexpr uint32_t INV30 = 0x2A774EC1u;
+};
+struct ModP {
+  static constexpr int32_t L[9] = {0x3FFFFC2F, 0x3FFFFFFB, 0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF,
+                                   0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0xFFFF};
+  static constexpr uint32_t INV30 = 0x2DDACACFu;
+};
 
 // u256 (8 little-endian words) -> signed30
 HKV_HD void to30(int32_t r[9], const uint32_t a[8]) {
@@ -102,8 +116,9 @@ HKV_HD void update_fg(int32_t f[9], int32_t g[9], const int32_t t[4]) {
   g[8] = (int32_t)cg;
 }
 
-// (d, e) <- t (d, e) / 2^30 (mod n), adding multiples of n to make the
-// division exact; keeps d, e in (-2n, n).
+// (d, e) <- t (d, e) / 2^30 (mod m), adding multiples of m to make the
+// division exact; keeps d, e in (-2m, m).
+template <class M>
 HKV_HD void update_de(int32_t d[9], int32_t e[9], const int32_t t[4]) {
   const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
   const int32_t sd = d[8] >> 31, se = e[8] >> 31;
@@ -111,16 +126,16 @@ HKV_HD void update_de(int32_t d[9], int32_t e[9], const int32_t t[4]) {
   int32_t me = (q & sd) + (r & se);
   int64_t cd = (int64_t)u * d[0] + (int64_t)v * e[0];
   int64_t ce = (int64_t)q * d[0] + (int64_t)r * e[0];
-  md -= (int32_t)((NINV30 * (uint32_t)cd + (uint32_t)md) & M30);
-  me -= (int32_t)((NINV30 * (uint32_t)ce + (uint32_t)me) & M30);
-  cd += (int64_t)NL[0] * md;
-  ce += (int64_t)NL[0] * me;
+  md -= (int32_t)((M::INV30 * (uint32_t)cd + (uint32_t)md) & M30);
+  me -= (int32_t)((M::INV30 * (uint32_t)ce + (uint32_t)me) & M30);
+  cd += (int64_t)M::L[0] * md;
+  ce += (int64_t)M::L[0] * me;
   cd >>= 30;
   ce >>= 30;
 #pragma unroll
   for (int i = 1; i < 9; ++i) {
-    cd += (int64_t)u * d[i] + (int64_t)v * e[i] + (int64_t)NL[i] * md;
-    ce += (int64_t)q * d[i] + (int64_t)r * e[i] + (int64_t)NL[i] * me;
+    cd += (int64_t)u * d[i] + (int64_t)v * e[i] + (int64_t)M::L[i] * md;
+    ce += (int64_t)q * d[i] + (int64_t)r * e[i] + (int64_t)M::L[i] * me;
     d[i - 1] = (int32_t)((uint32_t)cd & M30);
     e[i - 1] = (int32_t)((uint32_t)ce & M30);
     cd >>= 30;
@@ -130,12 +145,13 @@ HKV_HD void update_de(int32_t d[9], int32_t e[9], const int32_t t[4]) {
   e[8] = (int32_t)ce;
 }
 
-// r = a^-1 mod n for 0 < a < n (a = 0 gives 0).
-HKV_HD void inv_mod_n(uint32_t out[8], const uint32_t a[8]) {
+// r = a^-1 mod m for 0 < a < m (a = 0 gives 0).
+template <class M>
+HKV_HD void inv_mod(uint32_t out[8], const uint32_t a[8]) {
   int32_t f[9], g[9], d[9], e[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    f[i] = NL[i];
+    f[i] = M::L[i];
     d[i] = 0;
     e[i] = 0;
   }
@@ -147,7 +163,7 @@ HKV_HD void inv_mod_n(uint32_t out[8], const uint32_t a[8]) {
     int32_t t[4];
     delta = divsteps30(delta, (uint32_t)f[0] | ((uint32_t)f[1] << 30), (uint32_t)g[0] | ((uint32_t)g[1] << 30), t);
     update_fg(f, g, t);
-    update_de(d, e, t);
+    update_de<M>(d, e, t);
   }
   // f = ±1: result = d * f, then into [0, n): d in (-2n, 2n)
   const int32_t fneg = f[8] >> 31;
@@ -165,22 +181,22 @@ HKV_HD void inv_mod_n(uint32_t out[8], const uint32_t a[8]) {
     c = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      c += (int64_t)d[i] + (NL[i] & neg);
+      c += (int64_t)d[i] + (M::L[i] & neg);
       d[i] = (int32_t)((uint32_t)c & M30);
       c >>= 30;
     }
-    d[8] = (int32_t)(c + d[8] + (NL[8] & neg));
+    d[8] = (int32_t)(c + d[8] + (M::L[8] & neg));
   }
   {  // subtract n once if d >= n: compute d - n, keep it when non-negative
     int32_t s[9];
     c = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      c += (int64_t)d[i] - NL[i];
+      c += (int64_t)d[i] - M::L[i];
       s[i] = (int32_t)((uint32_t)c & M30);
       c >>= 30;
     }
-    s[8] = (int32_t)(c + d[8] - NL[8]);
+    s[8] = (int32_t)(c + d[8] - M::L[8]);
     const int32_t keep = ~(s[8] >> 31);  // all ones when d - n >= 0
 #pragma unroll
     for (int i = 0; i < 9; ++i) d[i] = (s[i] & keep) | (d[i] & ~keep);
@@ -195,6 +211,9 @@ HKV_HD void inv_mod_n(uint32_t out[8], const uint32_t a[8]) {
   out[6] = ((uint32_t)d[6] >> 12) | ((uint32_t)d[7] << 18);
   out[7] = ((uint32_t)d[7] >> 14) | ((uint32_t)d[8] << 16);
 }
+
+HKV_HD void inv_mod_n(uint32_t out[8], const uint32_t a[8]) { inv_mod<ModN>(out, a); }
+HKV_HD void inv_mod_p(uint32_t out[8], const uint32_t a[8]) { inv_mod<ModP>(out, a); }
 
 }  // namespace sgcd
 }  // namespace hkv

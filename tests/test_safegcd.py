@@ -1,6 +1,7 @@
-"""Host build of the device safegcd scalar inversion (hkv_safegcd.h, used by
-hkv_inv_kernel for s^-1 mod n) against Python's pow(x, -1, n): the same
-source the kernel compiles, checked on edge and random scalars."""
+"""Host build of the device safegcd inversion (hkv_safegcd.h: s^-1 mod n in
+hkv_inv_kernel, den^-1 mod p in hkv_yverdict_kernel) against Python's
+pow(x, -1, m): the same source the kernels compile, checked on edge and
+random values."""
 import os
 import random
 import subprocess
@@ -19,9 +20,12 @@ def binary(tmp_path_factory):
     return out
 
 
-def run(binary, xs):
+P = 2**256 - 2**32 - 977
+
+
+def run(binary, xs, mod="n"):
     inp = "".join(f"{x:064x}\n" for x in xs)
-    out = subprocess.run([binary], input=inp, capture_output=True, text=True, check=True).stdout.split()
+    out = subprocess.run([binary, mod], input=inp, capture_output=True, text=True, check=True).stdout.split()
     return [int(h, 16) for h in out]
 
 
@@ -45,3 +49,13 @@ def test_safegcd_random(binary):
 
 def test_safegcd_zero_maps_to_zero(binary):
     assert run(binary, [0]) == [0]
+
+
+def test_safegcd_mod_p(binary):
+    rng = random.Random(0x50)
+    xs = [1, 2, 3, P - 1, P - 2, (P - 1) // 2, 2**255, 2**32 + 977, 2**224, 0x3FFFFC2F, P - 2**32]
+    xs += [rng.randrange(1, P) for _ in range(20000)]
+    xs += [rng.getrandbits(rng.randrange(1, 256)) or 1 for _ in range(3000)]
+    xs += [P - (rng.getrandbits(rng.randrange(1, 128)) or 1) for _ in range(3000)]
+    for x, r in zip(xs, run(binary, xs, "p")):
+        assert r == pow(x, -1, P), hex(x)

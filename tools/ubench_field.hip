@@ -208,6 +208,22 @@ __global__ void check_chains(uint32_t* bad) {
   for (int k = 0; k < 64; ++k) fe_sqr_ref(s, s);
   fe_normalize(r); fe_normalize(s);
   nb += 2 * !fe_eq_norm(r, s);
+  // fe_cneg against fe_neg + select, on random, zero, p and weak-form values >= p
+  for (int e = 0; e < 6; ++e) {
+    fe b = a;
+    if (e == 1) fe_set_zero(b);
+    if (e == 2 || e == 3) { b.v[0] = 0xFFFFFC2Fu + (e == 3 ? 5u : 0u); b.v[1] = 0xFFFFFFFEu; for (int q = 2; q < 8; ++q) b.v[q] = 0xFFFFFFFFu; }
+    if (e == 4) for (int q = 0; q < 8; ++q) b.v[q] = 0xFFFFFFFFu;
+    if (e == 5) { fe_set_zero(b); b.v[1] = 0xFFFFFFFFu; b.v[0] = tid; }
+    for (int ng = 0; ng < 2; ++ng) {
+      fe x, y;
+      fe_cneg(x, b, ng != 0);
+      fe_neg(y, b);
+      if (ng == 0) y = b;
+      fe_normalize(x); fe_normalize(y);
+      nb += 8 * !fe_eq_norm(x, y);
+    }
+  }
   fe_mul(r, a, a); fe_mul(r, r, a); fe_sqr(r, r); fe_mul(r, a, r);
   fe_mul_ref(s, a, a); fe_mul_ref(s, s, a); fe_sqr_ref(s, s); fe_mul_ref(s, a, s);
   fe_normalize(r); fe_normalize(s);
@@ -280,7 +296,7 @@ int main() {
     hipMemset(bad, 0, 4);
     hipLaunchKernelGGL(check_chains, dim3(64), dim3(256), 0, 0, bad);
     hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
-    printf("{\"check\": \"fe_inv / 64 squarings / mixed chain vs the reference ops (bit mask of failing checks)\", \"lanes\": %d, \"fail_mask\": %u}\n", 64 * 256, hb);
+    printf("{\"check\": \"fe_inv / 64 squarings / cneg / mixed chain vs the reference ops (bit mask of failing checks)\", \"lanes\": %d, \"fail_mask\": %u}\n", 64 * 256, hb);
     hipFree(bad);
   }
   for (int bpc : {1, 2, 4}) {
