@@ -28,8 +28,8 @@ namespace hkv {
 hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im, bool split,
                            hipStream_t st);
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, unsigned long long* clk,
-                         uint32_t* rare_ctr, hipStream_t st);
+                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
+                         unsigned long long* clk, uint32_t* rare_ctr, hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 // y-free full-grid batches (HKV_YFREE): u1 * G, the y0 = num / den reduction and the verdict bitmap
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,

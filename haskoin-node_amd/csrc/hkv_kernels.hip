@@ -501,8 +501,12 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
 #ifndef HKV_FUSE_FINISH
 #define HKV_FUSE_FINISH 0
 #endif
-template <bool SPLIT>
-__global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
+// ILP: the paired-product group forms. The split kernel uses them (< 1 wave
+// per SIMD); full-grid launches of mid-size batches (at most 2 waves per
+// SIMD: 32k-131k signatures) take the <false, true> instance, which is
+// allocated for 2 waves per SIMD (no spill).
+template <bool SPLIT, bool ILP>
+__global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_ECMULT_WAVES)) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits, uint32_t n_words,
@@ -659,7 +663,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
       if (win != NWIN - 1) {
 #pragma unroll 1
         for (int d = 0; d < QW; ++d) {
-          if (!inf) ec_double<SPLIT && HKV_SPLIT_ILP>(acc);
+          if (!inf) ec_double<ILP>(acc);
         }
       }
       // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
@@ -684,7 +688,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
         fe_cmov(ty, nty, neg);
 #endif
         const bool was_inf = inf;
-        ec_accumulate<SPLIT && HKV_SPLIT_ILP>(acc, inf, acc.z, tx, ty, take);
+        ec_accumulate<ILP>(acc, inf, acc.z, tx, ty, take);
         // only the first nonzero digit of a lane starts from infinity: skip
         // the 24 selects in every window where no lane of the wave does
         if (__any(take && was_inf)) gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
@@ -717,7 +721,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : HKV_ECMULT_WAVES
           fe az;
           fe_mul(az, acc.z, Zg);
           const bool was_inf = inf;
-          ec_accumulate<SPLIT && HKV_SPLIT_ILP>(acc, inf, az, tx, ty, take);
+          ec_accumulate<ILP>(acc, inf, az, tx, ty, take);
           if (__any(take && was_inf)) {  // map the G-multiple onto the accumulator's curve
             fe zg2;
             fe_sqr(zg2, Zg);
@@ -1503,15 +1507,21 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
+#ifndef HKV_MID_ILP
+#define HKV_MID_ILP 1  // mid-size full-grid batches use the paired forms
+#endif
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, unsigned long long* clk,
-                         uint32_t* rare_ctr, hipStream_t st) {
+                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
+                         unsigned long long* clk, uint32_t* rare_ctr, hipStream_t st) {
   if (split)
-    hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, n_words,
-                       clk, rare_ctr);
+    hipLaunchKernelGGL((hkv_ecmult_kernel<true, HKV_SPLIT_ILP != 0>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab,
+                       qs, bits, n_words, clk, rare_ctr);
+  else if (ilp && HKV_MID_ILP)
+    hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
+                       n_words, clk, rare_ctr);
   else
-    hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits, n_words,
-                       clk, rare_ctr);
+    hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
+                       n_words, clk, rare_ctr);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {
@@ -1536,8 +1546,13 @@ hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
   hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad, (const uint32_t*)rare_ctr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // VERDICT_BATCH signatures per lane, the stride a multiple of WG (n_pad is)
-  const uint32_t stride = ceil_div(ceil_div(n_pad, VERDICT_BATCH), WG) * WG;
+  // VERDICT_BATCH signatures per lane at large n; smaller batches keep at
+  // least 65,536 lanes (or one per signature), as the s^-1 kernel does, so
+  // the per-lane inversion's latency is not serialised over 16 signatures.
+  // The stride is a multiple of WG (n_pad is).
+  uint32_t stride = ceil_div(ceil_div(n_pad, VERDICT_BATCH), WG) * WG;
+  const uint32_t min_lanes = n_pad < 65536u ? n_pad : 65536u;
+  if (stride < min_lanes) stride = min_lanes;
   hipLaunchKernelGGL(hkv_yverdict_kernel, dim3(stride / WG), dim3(WG), 0, st, im, n_pad, stride, bits, n_words,
                      rare_ctr);
   return hipGetLastError();
@@ -1572,7 +1587,7 @@ hipError_t launch_gen_sign(uint64_t seed, uint32_t n, const uint8_t* priv, const
   return hipGetLastError();
 }
 hipError_t ecmult_max_blocks_per_cu(int* out) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel<false>, WG, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel<false, false>, WG, 0);
 }
 
 }  // namespace hkv
