@@ -930,16 +930,29 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
   // ---- A = u1 * G: one affine addition per window, table t = 2j + h holds
   // multiples of 2^(GTAB_W j + 128 h) G; the next entry is loaded before
   // the current addition
+  // (window 0 starts the sum: A = its entry, affine, without an addition)
   gej A;
-  bool ainf = true;
-  fe_set_zero(A.x);
-  fe_set_zero(A.y);
-  fe_set_zero(A.z);
+  bool ainf;
   uint32_t gd = valid ? im[(size_t)IM_GDIG * n_pad + i] : 0u;
   fe tx, ty;
   gtab_entry(gtab, 0, gd, tx, ty);
+#if HKV_CNEG
+  fe_cneg(A.y, ty, (gd & GD_NEG) != 0);
+#else
+  {
+    fe nty;
+    fe_neg(nty, ty);
+    A.y = ty;
+    fe_cmov(A.y, nty, (gd & GD_NEG) != 0);
+  }
+#endif
+  A.x = tx;
+  fe_set_u32(A.z, 1);
+  ainf = (gd & GD_MAG) == 0;
+  gd = valid ? im[(size_t)(IM_GDIG + 1) * n_pad + i] : 0u;
+  gtab_entry(gtab, 1, gd, tx, ty);
 #pragma unroll 1
-  for (int t = 0; t < 2 * GWIN; ++t) {
+  for (int t = 1; t < 2 * GWIN; ++t) {
     const uint32_t gdn = (t + 1 < 2 * GWIN && valid) ? im[(size_t)(IM_GDIG + t + 1) * n_pad + i] : 0u;
     fe nx, nyy;
     if (t + 1 < 2 * GWIN) gtab_entry(gtab, t + 1, gdn, nx, nyy);

@@ -58,7 +58,10 @@ constexpr uint32_t DIG_ZERO = (uint32_t)QBIAS | ((uint32_t)QBIAS << QDIG_BITS);
 
 // signatures per thread in the scalar kernel (one s^-1 per BATCH_INV via
 // Montgomery's trick: 3(B-1) multiplications + 1 inversion)
-constexpr int BATCH_INV = 16;
+#ifndef HKV_BATCH_INV
+#define HKV_BATCH_INV 16
+#endif
+constexpr int BATCH_INV = HKV_BATCH_INV;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
 // y-free verification (HKV_YFREE, full-grid batches; hkv_kernels.hip §2b):
