@@ -907,8 +907,9 @@ constexpr int VERDICT_BATCH = HKV_VERDICT_BATCH;
 #define HKV_VERDICT_SAFEGCD 1
 #endif
 #ifndef HKV_FINISH_WAVES
-#define HKV_FINISH_WAVES 2  // waves per SIMD the finish kernel's register allocation targets (4: 179 VGPRs
-                            // spilled, 1-2% slower in the same-box A/B)
+#define HKV_FINISH_WAVES 3  // waves per SIMD the finish kernel's register allocation targets: 3 (168 VGPRs,
+                            // 180 B/lane spilled) is 0.8% faster than 2 (208 VGPRs), 4 (179 VGPRs spilled)
+                            // 1-2% slower (profiles/r02_variants_finish_waves.log, r02_variants_yfree.log)
 #endif
 HKV_DEV void gtab_entry(const uint32_t* __restrict__ gtab, int t, uint32_t gd, fe& tx, fe& ty) {
   const uint32_t mag = gd & GD_MAG;
