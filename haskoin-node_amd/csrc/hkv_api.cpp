@@ -158,11 +158,15 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
           "prologue launch");
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
-  const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
-                                : (uint32_t)std::min<size_t>(n_pad / hkv::WG, d.grid_max);
   // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
   // instance, every block resident at its 2-wave allocation
-  const bool ilp = !split && n_pad <= (size_t)d.grid_max * hkv::WG / 2;
+  // (HKV_ILP_ALL: every full-grid batch on the paired-form instance, 2 waves/SIMD)
+#ifndef HKV_ILP_ALL
+#define HKV_ILP_ALL 0
+#endif
+  const bool ilp = !split && (HKV_ILP_ALL || n_pad <= (size_t)d.grid_max * hkv::WG / 2);
+  const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
+                                : (uint32_t)std::min<size_t>(n_pad / hkv::WG, ilp ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, ilp,
