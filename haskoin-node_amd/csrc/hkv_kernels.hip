@@ -262,42 +262,70 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
   }
 }
 
+// (at one wave per SIMD the loop is load-latency bound: each iteration's
+// operands are loaded one iteration ahead)
 __global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t stride, uint32_t* __restrict__ im) {
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
   if (t >= stride) return;
   // forward: prefix products c_k = s_0 * ... * s_k (invalid lanes use s = 1)
   sc c;
   sc_set_u32(c, 1);
-#pragma unroll 1
-  for (int k = 0; k < BATCH_INV; ++k) {
-    const uint32_t i = t + (uint32_t)k * stride;
-    if (i >= n_pad) break;
+  int kn = 0;  // number of signatures of this lane
+  {
     sc sv;
-    im_load8(im, n_pad, IM_S, i, sv.v);
-    const bool valid = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_VALID) != 0;
-    if (!valid) sc_set_u32(sv, 1);
-    sc_mul(c, c, sv);
-    im_store8(im, n_pad, IM_C, i, c.v);
+    uint32_t fl = 0;
+    im_load8(im, n_pad, IM_S, t, sv.v);  // t < stride <= n_pad
+    fl = im[(size_t)IM_FLAGS * n_pad + t];
+#pragma unroll 1
+    for (int k = 0; k < BATCH_INV; ++k) {
+      const uint32_t i = t + (uint32_t)k * stride;
+      if (i >= n_pad) break;
+      kn = k + 1;
+      const uint32_t inext = i + stride;
+      sc sn;
+      uint32_t fn = 0;
+      if (k + 1 < BATCH_INV && inext < n_pad) {
+        im_load8(im, n_pad, IM_S, inext, sn.v);
+        fn = im[(size_t)IM_FLAGS * n_pad + inext];
+      }
+      if (!(fl & FLAG_VALID)) sc_set_u32(sv, 1);
+      sc_mul(c, c, sv);
+      im_store8(im, n_pad, IM_C, i, c.v);
+      sv = sn;
+      fl = fn;
+    }
   }
   sc inv;
   sc_inv(inv, c);
   // backward: s_k^-1 = inv * c_{k-1} (stored over c_k); inv *= s_k
-#pragma unroll 1
-  for (int k = BATCH_INV - 1; k >= 0; --k) {
-    const uint32_t i = t + (uint32_t)k * stride;
-    if (i >= n_pad) continue;
-    const bool valid = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_VALID) != 0;
-    sc prev, sv, sinv;
-    if (k > 0) {
-      im_load8(im, n_pad, IM_C, i - stride, prev.v);
-    } else {
-      sc_set_u32(prev, 1);
-    }
-    sc_mul(sinv, inv, prev);
-    im_store8(im, n_pad, IM_C, i, sinv.v);
+  if (kn == 0) return;
+  {
+    int k = kn - 1;
+    uint32_t i = t + (uint32_t)k * stride;
+    sc prev, sv;
+    uint32_t fl = im[(size_t)IM_FLAGS * n_pad + i];
     im_load8(im, n_pad, IM_S, i, sv.v);
-    if (!valid) sc_set_u32(sv, 1);
-    sc_mul(inv, inv, sv);
+    if (k > 0) im_load8(im, n_pad, IM_C, i - stride, prev.v);
+#pragma unroll 1
+    for (; k >= 0; --k) {
+      i = t + (uint32_t)k * stride;
+      sc pn, sn;
+      uint32_t fn = 0;
+      if (k > 0) {  // the next (lower) signature's operands
+        fn = im[(size_t)IM_FLAGS * n_pad + i - stride];
+        im_load8(im, n_pad, IM_S, i - stride, sn.v);
+        if (k > 1) im_load8(im, n_pad, IM_C, i - 2 * stride, pn.v);
+      }
+      if (k == 0) sc_set_u32(prev, 1);
+      sc sinv;
+      sc_mul(sinv, inv, prev);
+      im_store8(im, n_pad, IM_C, i, sinv.v);
+      if (!(fl & FLAG_VALID)) sc_set_u32(sv, 1);
+      sc_mul(inv, inv, sv);
+      prev = pn;
+      sv = sn;
+      fl = fn;
+    }
   }
 }
 
@@ -1128,18 +1156,33 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
                                                           uint32_t* __restrict__ rare_ctr) {
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
   if (t == 0) *rare_ctr = 0;  // re-arm for the next batch (the rare kernel has read it)
+  // one wave per SIMD at 1M: the loops are load-latency bound, so each
+  // iteration's operands are loaded one iteration ahead
   fe c;
   fe_set_u32(c, 1);
-#pragma unroll 1
-  for (int k = 0; k < VERDICT_BATCH; ++k) {
-    const uint32_t i = t + (uint32_t)k * stride;
-    if (i >= n_pad) break;
-    const bool decided = (im[(size_t)IM_FLAGS * n_pad + i] & FLAG_DECIDED) != 0;
+  int kn = 0;
+  {
     fe d;
-    im_load8(im, n_pad, IM_DEN, i, d.v);
-    if (decided) fe_set_u32(d, 1);
-    fe_mul(c, c, d);
-    im_store8(im, n_pad, IM_C, i, c.v);
+    im_load8(im, n_pad, IM_DEN, t, d.v);  // t < stride <= n_pad
+    uint32_t fl = im[(size_t)IM_FLAGS * n_pad + t];
+#pragma unroll 1
+    for (int k = 0; k < VERDICT_BATCH; ++k) {
+      const uint32_t i = t + (uint32_t)k * stride;
+      if (i >= n_pad) break;
+      kn = k + 1;
+      const uint32_t inext = i + stride;
+      fe dn;
+      uint32_t fn = 0;
+      if (k + 1 < VERDICT_BATCH && inext < n_pad) {
+        im_load8(im, n_pad, IM_DEN, inext, dn.v);
+        fn = im[(size_t)IM_FLAGS * n_pad + inext];
+      }
+      if (fl & FLAG_DECIDED) fe_set_u32(d, 1);
+      fe_mul(c, c, d);
+      im_store8(im, n_pad, IM_C, i, c.v);
+      d = dn;
+      fl = fn;
+    }
   }
   fe inv;
 #if HKV_VERDICT_SAFEGCD
@@ -1148,44 +1191,54 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
 #else
   fe_inv(inv, c);
 #endif
-#pragma unroll 1
-  for (int k = VERDICT_BATCH - 1; k >= 0; --k) {
+  struct Ops {
+    uint32_t f;
+    fe prev, d, num, w;
+    uint32_t r[8];
+  };
+  auto load_ops = [&](Ops& o, int k) {
     const uint32_t i = t + (uint32_t)k * stride;
-    if (i >= n_pad) continue;  // wave-uniform: n_pad and stride are multiples of 64
-    const uint32_t f = im[(size_t)IM_FLAGS * n_pad + i];
+    o.f = im[(size_t)IM_FLAGS * n_pad + i];
+    if (k > 0) im_load8(im, n_pad, IM_C, i - stride, o.prev.v);
+    im_load8(im, n_pad, IM_DEN, i, o.d.v);
+    im_load8(im, n_pad, IM_NUM, i, o.num.v);
+    im_load8(im, n_pad, IM_W, i, o.w.v);
+    im_load8(im, n_pad, IM_R, i, o.r);
+  };
+  Ops cur;
+  if (kn > 0) load_ops(cur, kn - 1);
+#pragma unroll 1
+  for (int k = kn - 1; k >= 0; --k) {
+    const uint32_t i = t + (uint32_t)k * stride;  // < n_pad; kn is wave-uniform (n_pad, stride multiples of 64)
+    Ops nxt;
+    if (k > 0) load_ops(nxt, k - 1);
+    const uint32_t f = cur.f;
     const bool decided = (f & FLAG_DECIDED) != 0;
-    fe prev, dinv, d;
-    if (k > 0) {
-      im_load8(im, n_pad, IM_C, i - stride, prev.v);
-    } else {
-      fe_set_u32(prev, 1);
-    }
-    fe_mul(dinv, inv, prev);
-    im_load8(im, n_pad, IM_DEN, i, d.v);
-    if (decided) fe_set_u32(d, 1);
-    fe_mul(inv, inv, d);
+    fe dinv;
+    if (k == 0) fe_set_u32(cur.prev, 1);
+    fe_mul(dinv, inv, cur.prev);
+    if (decided) fe_set_u32(cur.d, 1);
+    fe_mul(inv, inv, cur.d);
     bool accept = (f & FLAG_ACCEPT) != 0;
     if (!decided) {
-      fe num, w, yc, y2;
-      uint32_t r[8];
-      im_load8(im, n_pad, IM_NUM, i, num.v);
-      im_load8(im, n_pad, IM_W, i, w.v);
-      im_load8(im, n_pad, IM_R, i, r);
+      fe yc, y2;
       const uint32_t want = (f & FLAG_YODD) ? 1u : 0u;
-      fe_mul(yc, num, dinv);
+      fe_mul(yc, cur.num, dinv);
       fe_normalize(yc);
       fe_sqr(y2, yc);
-      bool ok = fe_equal(y2, w) && (yc.v[0] & 1u) == want;
-      const bool small_r = u256_lt(r, PMN);
+      bool ok = fe_equal(y2, cur.w) && (yc.v[0] & 1u) == want;
+      const bool small_r = u256_lt(cur.r, PMN);
       if (__any(!ok && small_r)) {
-        im_load8(im, n_pad, IM_NUM + 8, i, num.v);
-        fe_mul(yc, num, dinv);
+        fe numn;
+        im_load8(im, n_pad, IM_NUM + 8, i, numn.v);
+        fe_mul(yc, numn, dinv);
         fe_normalize(yc);
         fe_sqr(y2, yc);
-        ok = ok || (small_r && fe_equal(y2, w) && (yc.v[0] & 1u) == want);
+        ok = ok || (small_r && fe_equal(y2, cur.w) && (yc.v[0] & 1u) == want);
       }
       accept = ok;
     }
+    cur = nxt;
     const uint64_t ball = __ballot(accept);
     if ((threadIdx.x & 63) == 0) {
       const uint32_t wi = i / 32;
