@@ -21,10 +21,13 @@ from collections import defaultdict
 
 
 def kname(raw: str) -> str:
-    """hkv::hkv_ecmult_kernel<false>(...) -> hkv_ecmult_kernel; <true> -> _split."""
+    """hkv::hkv_ecmult_kernel<false, false>(...) -> hkv_ecmult_kernel; <false, true> -> _mid; <true, ...> -> _split."""
     k = raw.split("(")[0].replace("hkv::", "")
     if k.startswith("void "):
         k = k[5:]
+    # hkv_ecmult_kernel<SPLIT, ILP>: <false, false> full grid, <false, true> mid-size, <true, *> split
+    k = k.replace("<false, false>", "").replace("<false, true>", "_mid")
+    k = k.replace("<true, true>", "_split").replace("<true, false>", "_split")
     return k.replace("<false>", "").replace("<true>", "_split")
 
 
