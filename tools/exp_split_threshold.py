@@ -16,7 +16,7 @@ def main():
     st = torch.cuda.Stream()
     sp = st.cuda_stream
     out = {}
-    for n in (16384, 32768, 49152, 65536, 98304):
+    for n in (8192, 16384, 24576, 32768, 49152, 65536, 98304, 131072):
         recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
         bits = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
         v.gen_records_device(0, 77 + n, n, 65536, 100, recs.data_ptr(), sp)
