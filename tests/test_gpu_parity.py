@@ -153,16 +153,18 @@ def test_golden_kat_every_offset(ver, kat):
         assert (got == exp).all()
 
 
-def test_golden_kat_full_grid_yfree(ver, kat):
-    """Every golden KAT class through the full-grid (y-free) launch: the KATs
-    repeated in random order to 33,024 records (above the split bound, so the
-    prologue leaves w = x^3 + 7 and hkv_finish_kernel / hkv_rare_kernel /
-    hkv_yverdict_kernel decide), each verdict equal to its label in both
-    modes. Covers the rare paths (u1 = 0, sum = infinity, u1 G = +-u2 Q
-    collisions), non-residue and off-curve keys, and the r + n candidate."""
+@pytest.mark.parametrize("n", [(1 << 15) + 256, 139264])
+def test_golden_kat_full_grid_yfree(ver, kat, n):
+    """Every golden KAT class through the full-grid (y-free) launches: the
+    KATs repeated in random order to 33,024 records (the mid-size paired-form
+    ecmult instance) and 139,264 (the plain 4-wave instance) — above the split
+    bound, so the prologue leaves w = x^3 + 7 and hkv_finish_kernel /
+    hkv_rare_kernel / hkv_yverdict_kernel decide — each verdict equal to its
+    label in both modes. Covers the rare paths (u1 = 0, sum = infinity,
+    u1 G = +-u2 Q collisions), non-residue and off-curve keys, and the r + n
+    candidate."""
     recs, meta = kat
     rng = random.Random(11)
-    n = (1 << 15) + 256
     order = list(range(len(recs))) * (n // len(recs)) + [rng.randrange(len(recs)) for _ in range(n % len(recs))]
     rng.shuffle(order)
     arr = np.frombuffer(b"".join(recs[i] for i in order), dtype=np.uint8)
