@@ -1,18 +1,25 @@
 // hkv_kernels.hip — batch secp256k1 ECDSA verify kernels for gfx950.
 //
 // Pipeline per batch (one lane per signature, no MFMA: 256-bit integer work):
-//   1. hkv_prologue_kernel  — record parse (compact sig + SEC1 pubkey incl.
-//      hybrid keys and sqrt decompression), high-S policy, m = msg mod n,
-//      s^-1, u1 = m/s, u2 = r/s, GLV split of u2. Writes a SoA intermediate.
-//   2. hkv_ecmult_kernel    — per-lane table of 1..2^(QW-1) * Q (8 entries at the
-//      default radix 16) on an isomorphic
-//      curve (one common Z, so all Q additions are mixed), then a shared
-//      doubling chain of 132 bits with radix-16 Booth digits for k1*Q and
-//      k2*(lambda Q) and radix-2^20 Booth digits for u1_lo*G and
-//      u1_hi*(2^128 G) (G tables staged in LDS), then the inversion-free
-//      Jacobian x compare (r*Z^2 == X, and (r+n)*Z^2 == X when r < p-n).
-//      Verdicts leave as a ballot bitmap, one 64-bit word per wave.
-//   3. hkv_gtable_kernel    — once per context: the two fixed-base tables.
+//   1. hkv_prologue_kernel (+ hkv_inv_kernel, hkv_glv_kernel; small batches:
+//      hkv_prologue_split_kernel) — record parse (compact sig + SEC1 pubkey
+//      incl. hybrid keys; the sqrt decompression only on the split path),
+//      high-S policy, m = msg mod n, s^-1, u1 = m/s, u2 = r/s, GLV split of
+//      u2, Booth digits. Writes a SoA intermediate.
+//   2. hkv_ecmult_kernel<SPLIT, ILP> — per-lane table of 1..2^(QW-1) * Q (8
+//      entries at the default radix 16) on an isomorphic curve (one common Z,
+//      so all Q additions are mixed), then a shared doubling chain of 132
+//      bits with radix-16 Booth digits for k1*Q and k2*(lambda Q).
+//      Split (small-batch) launches also add radix-2^20 Booth digits of
+//      u1_lo*G and u1_hi*(2^128 G) (G entries staged in LDS) and end with the
+//      inversion-free Jacobian x compare (r*Z^2 == X, and (r+n)*Z^2 == X
+//      when r < p-n); verdicts leave as a ballot bitmap. Full-grid launches
+//      are y-free (section 2b): Q is taken on E_w (w = x^3 + 7, no sqrt) and
+//      B' = u2*Q' is handed to
+//   2b. hkv_finish_kernel, hkv_rare_kernel, hkv_yverdict_kernel — u1*G from
+//      per-window tables, y0 = num/den from "x(u1 G + u2 Q) == r", and the
+//      verdict "y_c^2 == w with the key's parity" (rare lanes: exact sqrt path).
+//   3. hkv_gtable_kernel    — once per context: the fixed-base tables.
 //   4. hkv_gen_*            — synthetic valid batches (keyless construction,
 //      SURVEY.md §8(c)) for the benchmark and the tests.
 //
