@@ -59,6 +59,11 @@ struct DevCtx {
   uint64_t* ms_total_dev = nullptr;  // its device-side address
   void* ms_ctr = nullptr;            // device counters of hkv_ms_scan_kernel
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
+  // split y-free (HKV_SPLIT_YFREE): hkv_gsqrt_kernel's stream, its output and the two ordering events
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t ev_pro = nullptr, ev_aux = nullptr;
+  uint32_t* aux = nullptr;
+  size_t aux_n = 0;                  // signatures aux holds (the split bound)
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -157,6 +162,22 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
   HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
           "prologue launch");
+  const bool split_yf = split && HKV_SPLIT_YFREE;
+  if (split_yf) {  // u1 * G and the key's square root beside the split ecmult
+    if (d.aux_n < n_pad) {
+      if (d.aux) {
+        HKV_TRY(hipStreamSynchronize(d.aux_stream), "aux sync");
+        (void)hipFree(d.aux);
+        d.aux = nullptr;
+      }
+      HKV_TRY(hipMalloc(&d.aux, n_pad * hkv::AUX_WORDS * sizeof(uint32_t)), "hipMalloc(aux)");
+      d.aux_n = n_pad;
+    }
+    HKV_TRY(hipEventRecord(d.ev_pro, st), "hipEventRecord(aux)");
+    HKV_TRY(hipStreamWaitEvent(d.aux_stream, d.ev_pro, 0), "hipStreamWaitEvent(aux)");
+    HKV_TRY(hkv::launch_gsqrt(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.aux, d.aux_stream), "gsqrt launch");
+    HKV_TRY(hipEventRecord(d.ev_aux, d.aux_stream), "hipEventRecord(aux)");
+  }
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
   // instance, every block resident at its 2-wave allocation
@@ -176,6 +197,10 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)
   if (!split && HKV_YFREE) HKV_TRY(hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st),
                                    "finish launch");
+  if (split_yf) {
+    HKV_TRY(hipStreamWaitEvent(st, d.ev_aux, 0), "hipStreamWaitEvent(join)");
+    HKV_TRY(hkv::launch_split_join(d.im, (uint32_t)n, (uint32_t)n_pad, d.aux, vbits, n_words, st), "join launch");
+  }
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
     d.ev.insert(d.ev.end(), e, e + 3);
@@ -207,6 +232,9 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
   HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
+  HKV_TRY(hipStreamCreateWithFlags(&d.aux_stream, hipStreamNonBlocking), "hipStreamCreate(aux)");
+  HKV_TRY(hipEventCreateWithFlags(&d.ev_pro, hipEventDisableTiming), "hipEventCreate(aux)");
+  HKV_TRY(hipEventCreateWithFlags(&d.ev_aux, hipEventDisableTiming), "hipEventCreate(aux)");
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
@@ -248,6 +276,10 @@ void free_device(DevCtx& d) {
   if (d.ms_total) (void)hipHostFree(d.ms_total);
   if (d.ms_ctr) (void)hipFree(d.ms_ctr);
   if (d.rare_ctr) (void)hipFree(d.rare_ctr);
+  if (d.aux) (void)hipFree(d.aux);
+  if (d.ev_pro) (void)hipEventDestroy(d.ev_pro);
+  if (d.ev_aux) (void)hipEventDestroy(d.ev_aux);
+  if (d.aux_stream) (void)hipStreamDestroy(d.aux_stream);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.clk) (void)hipFree(d.clk);
   if (d.last_use) (void)hipEventDestroy(d.last_use);

@@ -389,13 +389,19 @@ __global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* 
       for (int k = 24; k < 42; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
     }
     fe x, y;
+#if HKV_SPLIT_YFREE
+    uint32_t pflags = 0;  // y stays implicit: IM_QY = w (the square root runs beside the ecmult)
+    const bool pk = pubkey_parse_rec_w(w, x, y, pflags) && i < n;
+#else
+    const uint32_t pflags = 0;
     const bool pk = pubkey_parse_rec(w, x, y) && i < n;
+#endif
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       im[(size_t)(IM_QX + k) * n_pad + i] = x.v[k];
       im[(size_t)(IM_QY + k) * n_pad + i] = y.v[k];
     }
-    pk_ok_s[sub] = pk ? 1u : 0u;
+    pk_ok_s[sub] = (pk ? 1u : 0u) | pflags;
   } else {
     if (i < n) {
 #pragma unroll
@@ -436,7 +442,8 @@ __global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* 
   __syncthreads();
   if (half == 1) {
     // flags as the three-kernel path leaves them (hkv_glv_kernel)
-    uint32_t f = (ok && pk_ok_s[sub]) ? FLAG_VALID : 0u;
+    uint32_t f = (ok && (pk_ok_s[sub] & 1u)) ? FLAG_VALID : 0u;
+    f |= pk_ok_s[sub] & (FLAG_YODD | FLAG_COMP);
     f |= (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
     if (!glv_ok) f &= ~FLAG_VALID;
     im[(size_t)IM_FLAGS * n_pad + i] = f;
@@ -580,8 +587,8 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_E
       q.x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
       q.y.v[k] = im[(size_t)(IM_QY + k) * n_pad + i];
     }
-#if HKV_YFREE
-    if (!SPLIT) {  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
+#if HKV_YFREE || HKV_SPLIT_YFREE
+    if (SPLIT ? HKV_SPLIT_YFREE : HKV_YFREE) {  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
       fe xw, ww;
       fe_mul(xw, q.x, q.y);
       fe_sqr(ww, q.y);
@@ -676,7 +683,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_E
       const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
       // y-free full-grid launches leave u1 * G to the finish kernel
-      const bool gwin = (SPLIT || !HKV_YFREE) && (win % GSTEP) == 0;
+      const bool gwin = (SPLIT ? !HKV_SPLIT_YFREE : !HKV_YFREE) && (win % GSTEP) == 0;
       uint32_t gd0 = 0, gd1 = 0;
       if (gwin) {
         const int gj = win / GSTEP;
@@ -815,19 +822,21 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_E
       __syncthreads();  // the next window loop's G DMA reuses gpf
     }
 
-#if HKV_YFREE
-    if (!SPLIT) {  // hand B' = (X, Y, Z acc * Zg) on E_w to the finish kernel
-      fe zt;
-      fe_mul(zt, acc.z, Zg);
+#if HKV_YFREE || HKV_SPLIT_YFREE
+    if (SPLIT ? HKV_SPLIT_YFREE : HKV_YFREE) {  // hand B' = (X, Y, Z acc * Zg) on E_w on
+      if (!SPLIT || half == 0) {                 // (finish kernel / split join kernel)
+        fe zt;
+        fe_mul(zt, acc.z, Zg);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
-        im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
-        im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
+        for (int k = 0; k < 8; ++k) {
+          im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
+          im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
+          im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
+        }
+        im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
       }
-      im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
-#if HKV_FUSE_FINISH
-      finish_lane(im, n, n_pad, gtab, rare_ctr, i, flags | (inf ? FLAG_BINF : 0u));
+#if HKV_FUSE_FINISH && HKV_YFREE
+      if (!SPLIT) finish_lane(im, n, n_pad, gtab, rare_ctr, i, flags | (inf ? FLAG_BINF : 0u));
 #endif
       continue;
     }
@@ -956,19 +965,14 @@ HKV_DEV void gtab_entry(const uint32_t* __restrict__ gtab, int t, uint32_t gd, f
   ty.v[4] = a3.x; ty.v[5] = a3.y; ty.v[6] = a3.z; ty.v[7] = a3.w;
 }
 
-// one signature's finish (hkv_finish_kernel, or the ecmult kernel's own
-// tail with HKV_FUSE_FINISH): whole waves call it (the rare-lane compaction
-// ballots)
-HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
-                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags) {
-  const bool valid = (i < n) && (flags & FLAG_VALID);
-
+// A = u1 * G of signature i: one affine addition per window, from the
+// per-window tables (no doublings)
+HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab, uint32_t i,
+                       bool valid, gej& A, bool& ainf) {
   // ---- A = u1 * G: one affine addition per window, table t = 2j + h holds
   // multiples of 2^(GTAB_W j + 128 h) G; the next entry is loaded before
   // the current addition
   // (window 0 starts the sum: A = its entry, affine, without an addition)
-  gej A;
-  bool ainf;
   uint32_t gd = valid ? im[(size_t)IM_GDIG * n_pad + i] : 0u;
   fe tx, ty;
   gtab_entry(gtab, 0, gd, tx, ty);
@@ -1007,6 +1011,18 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
     tx = nx;
     ty = nyy;
   }
+}
+
+// one signature's finish (hkv_finish_kernel, or the ecmult kernel's own
+// tail with HKV_FUSE_FINISH): whole waves call it (the rare-lane compaction
+// ballots)
+HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
+                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags) {
+  const bool valid = (i < n) && (flags & FLAG_VALID);
+
+  gej A;
+  bool ainf;
+  gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
 
   // ---- B' from the ecmult kernel, w, r (not hoisted above the loop: it
   // would hold 56 more VGPRs through every addition)
@@ -1254,6 +1270,75 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
     }
   }
 }
+#if HKV_SPLIT_YFREE
+// Small batches, y-free (HKV_SPLIT_YFREE): beside the split ecmult (which
+// leaves B' = u2 Q' on E_w), hkv_gsqrt_kernel runs on an auxiliary stream:
+// A = u1 G from the per-window tables and the key's y0 = sqrt(w) with the
+// key's parity (no root: the key does not parse). hkv_split_join_kernel then
+// maps B' back to E as (X, Y, Z y0) (phi^-1), adds A exactly and compares.
+// The square root thus leaves the small-batch critical path.
+__global__ void __launch_bounds__(WG) hkv_gsqrt_kernel(const uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
+                                                       const uint32_t* __restrict__ gtab, uint32_t* __restrict__ aux) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  const bool valid = (i < n) && (flags & FLAG_VALID);
+  gej A;
+  bool ainf;
+  gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
+  fe w, y0, y2, ny;
+  im_load8(im, n_pad, IM_W, i, w.v);
+  fe_sqrt_cand(y0, w);
+  fe_sqr(y2, y0);
+  const bool is_sq = fe_equal(y2, w);
+  fe_normalize(y0);
+  fe_neg(ny, y0);
+  fe_normalize(ny);
+  if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
+    aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
+    aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
+    aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
+  }
+  aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
+}
+
+__global__ void __launch_bounds__(WG) hkv_split_join_kernel(const uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
+                                                            const uint32_t* __restrict__ aux,
+                                                            uint32_t* __restrict__ bits, uint32_t n_words) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;  // n_pad % WG == 0: whole waves
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  const bool valid = (i < n) && (flags & FLAG_VALID);
+  gej A, B;
+  fe y0;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    B.x.v[k] = im[(size_t)(IM_BX + k) * n_pad + i];
+    B.y.v[k] = im[(size_t)(IM_BX + 8 + k) * n_pad + i];
+    B.z.v[k] = im[(size_t)(IM_BX + 16 + k) * n_pad + i];
+    A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
+    A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
+    A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
+    y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+    r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+  }
+  const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
+  gej b = B;
+  fe_mul(b.z, B.z, y0);  // B = phi^-1(B') = (X, Y, Z y0) on E
+  bool rinf = (af & AUXF_AINF) != 0;
+  gej_add_var(A, rinf, b, (flags & FLAG_BINF) != 0);
+  const bool accept = valid && (af & AUXF_SQ) && !rinf && x_matches_r(A.x, A.z, r);
+  const uint64_t ball = __ballot(accept);
+  if ((threadIdx.x & 63) == 0) {
+    const uint32_t wi = i / 32;
+    if (wi < n_words) bits[wi] = (uint32_t)ball;
+    if (wi + 1 < n_words) bits[wi + 1] = (uint32_t)(ball >> 32);
+  }
+}
+#endif
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1607,6 +1692,26 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
   hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div((size_t)GTAB_TABLES * GTAB_ENTRIES, WG)), dim3(WG), 0, st,
                      gtab);
   return hipGetLastError();
+}
+hipError_t launch_gsqrt(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* aux,
+                        hipStream_t st) {
+#if HKV_SPLIT_YFREE
+  hipLaunchKernelGGL(hkv_gsqrt_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, aux);
+  return hipGetLastError();
+#else
+  (void)im; (void)n; (void)n_pad; (void)gtab; (void)aux; (void)st;
+  return hipSuccess;
+#endif
+}
+hipError_t launch_split_join(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* aux, uint32_t* bits,
+                             uint32_t n_words, hipStream_t st) {
+#if HKV_SPLIT_YFREE
+  hipLaunchKernelGGL(hkv_split_join_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, aux, bits, n_words);
+  return hipGetLastError();
+#else
+  (void)im; (void)n; (void)n_pad; (void)aux; (void)bits; (void)n_words; (void)st;
+  return hipSuccess;
+#endif
 }
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st) {

@@ -73,6 +73,17 @@ constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF
 #ifndef HKV_YFREE
 #define HKV_YFREE 1
 #endif
+// Small batches (the split ecmult) y-free too (HKV_SPLIT_YFREE): the key's
+// square root leaves the prologue's critical path and runs beside the split
+// ecmult (hkv_gsqrt_kernel on an auxiliary stream, with the u1 * G sum);
+// hkv_split_join_kernel maps B' back with y0 and compares.
+#ifndef HKV_SPLIT_YFREE
+#define HKV_SPLIT_YFREE 1
+#endif
+static_assert(!HKV_SPLIT_YFREE || HKV_YFREE, "the split y-free path uses the y-free helpers and tables");
+// hkv_gsqrt_kernel's output (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
+enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_WORDS = 33 };
+constexpr uint32_t AUXF_AINF = 1u, AUXF_SQ = 2u;
 constexpr uint32_t FLAG_YODD = 16u;      // the key's y is odd (prefix 03/07, or the 04 key's y)
 constexpr uint32_t FLAG_COMP = 32u;      // compressed key: x^3 + 7 not yet shown to be a square
 constexpr uint32_t FLAG_BINF = 64u;      // B' = u2 * Q' is infinity
