@@ -232,9 +232,11 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
   HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
-  HKV_TRY(hipStreamCreateWithFlags(&d.aux_stream, hipStreamNonBlocking), "hipStreamCreate(aux)");
-  HKV_TRY(hipEventCreateWithFlags(&d.ev_pro, hipEventDisableTiming), "hipEventCreate(aux)");
-  HKV_TRY(hipEventCreateWithFlags(&d.ev_aux, hipEventDisableTiming), "hipEventCreate(aux)");
+  if (HKV_SPLIT_YFREE) {  // the split y-free path's auxiliary stream (off by default)
+    HKV_TRY(hipStreamCreateWithFlags(&d.aux_stream, hipStreamNonBlocking), "hipStreamCreate(aux)");
+    HKV_TRY(hipEventCreateWithFlags(&d.ev_pro, hipEventDisableTiming), "hipEventCreate(aux)");
+    HKV_TRY(hipEventCreateWithFlags(&d.ev_aux, hipEventDisableTiming), "hipEventCreate(aux)");
+  }
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");

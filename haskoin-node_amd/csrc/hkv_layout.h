@@ -76,9 +76,13 @@ constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF
 // Small batches (the split ecmult) y-free too (HKV_SPLIT_YFREE): the key's
 // square root leaves the prologue's critical path and runs beside the split
 // ecmult (hkv_gsqrt_kernel on an auxiliary stream, with the u1 * G sum);
-// hkv_split_join_kernel maps B' back with y0 and compares.
+// hkv_split_join_kernel maps B' back with y0 and compares. Correct (53/53
+// GPU tests) but off: the auxiliary stream's kernel is not reliably
+// concurrent with the split ecmult (configs[2] block 798 -> 772 us, configs[0]
+// block 754 -> 872 us; profiles/r02_variants_split_yfree.log); running it as
+// extra waves of the split kernel is the way to keep it concurrent.
 #ifndef HKV_SPLIT_YFREE
-#define HKV_SPLIT_YFREE 1
+#define HKV_SPLIT_YFREE 0
 #endif
 static_assert(!HKV_SPLIT_YFREE || HKV_YFREE, "the split y-free path uses the y-free helpers and tables");
 // hkv_gsqrt_kernel's output (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
