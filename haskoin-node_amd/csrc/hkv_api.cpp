@@ -162,17 +162,18 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
   HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
           "prologue launch");
-  const bool split_yf = split && HKV_SPLIT_YFREE;
-  if (split_yf) {  // u1 * G and the key's square root beside the split ecmult
-    if (d.aux_n < n_pad) {
-      if (d.aux) {
-        HKV_TRY(hipStreamSynchronize(d.aux_stream), "aux sync");
-        (void)hipFree(d.aux);
-        d.aux = nullptr;
-      }
-      HKV_TRY(hipMalloc(&d.aux, n_pad * hkv::AUX_WORDS * sizeof(uint32_t)), "hipMalloc(aux)");
-      d.aux_n = n_pad;
+  const bool split_yf = split && HKV_SPLIT_YFREE == 1;
+  if (split && HKV_SPLIT_YFREE && d.aux_n < n_pad) {  // A = u1 G, y0 (hkv_layout.h AUX_*)
+    if (d.aux) {
+      if (d.aux_stream) HKV_TRY(hipStreamSynchronize(d.aux_stream), "aux sync");
+      HKV_TRY(hipStreamSynchronize(st), "aux sync");
+      (void)hipFree(d.aux);
+      d.aux = nullptr;
     }
+    HKV_TRY(hipMalloc(&d.aux, n_pad * hkv::AUX_WORDS * sizeof(uint32_t)), "hipMalloc(aux)");
+    d.aux_n = n_pad;
+  }
+  if (split_yf) {  // u1 * G and the key's square root beside the split ecmult (aux stream)
     HKV_TRY(hipEventRecord(d.ev_pro, st), "hipEventRecord(aux)");
     HKV_TRY(hipStreamWaitEvent(d.aux_stream, d.ev_pro, 0), "hipStreamWaitEvent(aux)");
     HKV_TRY(hkv::launch_gsqrt(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.aux, d.aux_stream), "gsqrt launch");
@@ -191,7 +192,7 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, ilp,
-                             d.profile ? d.clk : nullptr, d.rare_ctr, st),
+                             d.profile ? d.clk : nullptr, d.rare_ctr, d.aux, st),
           "ecmult launch");
   // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
   // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)
@@ -232,7 +233,7 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
   HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
-  if (HKV_SPLIT_YFREE) {  // the split y-free path's auxiliary stream (off by default)
+  if (HKV_SPLIT_YFREE == 1) {  // the split y-free path's auxiliary stream (off by default)
     HKV_TRY(hipStreamCreateWithFlags(&d.aux_stream, hipStreamNonBlocking), "hipStreamCreate(aux)");
     HKV_TRY(hipEventCreateWithFlags(&d.ev_pro, hipEventDisableTiming), "hipEventCreate(aux)");
     HKV_TRY(hipEventCreateWithFlags(&d.ev_aux, hipEventDisableTiming), "hipEventCreate(aux)");

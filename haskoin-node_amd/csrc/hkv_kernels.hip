@@ -535,6 +535,10 @@ HKV_DEV void ec_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, cons
 #if HKV_YFREE
 HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
                          uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags);
+HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab, uint32_t i,
+                       bool valid, gej& A, bool& ainf);
+HKV_DEV void gej_add_var(gej& acc, bool& inf, const gej& b, bool binf);
+HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]);
 #endif
 // HKV_FUSE_FINISH: the full-grid ecmult kernel runs the finish (u1 * G, num,
 // den) itself after storing B', at its own occupancy, instead of a separate
@@ -548,12 +552,13 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
 // SIMD: 32k-131k signatures) take the <false, true> instance, which is
 // allocated for 2 waves per SIMD (no spill).
 template <bool SPLIT, bool ILP>
-__global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_ECMULT_WAVES)) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
+__global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_ECMULT_WAVES)) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                         uint32_t n_pad, const uint32_t* __restrict__ gtab,
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits, uint32_t n_words,
                                                         unsigned long long* __restrict__ clk,
-                                                        uint32_t* __restrict__ rare_ctr) {
+                                                        uint32_t* __restrict__ rare_ctr,
+                                                        uint32_t* __restrict__ aux) {
   // per wave: two G-entry slots (one in SPLIT mode: a wave adds one G term),
   // each 4 quads x 64 lanes x 16 B (LDS-DMA target); in SPLIT mode reused
   // after the window loop for the half-sum exchange
@@ -581,6 +586,38 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_E
     const uint32_t i = base + sub;
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
+#if HKV_SPLIT_YFREE == 2
+    if (SPLIT && half == 2) {
+      // waves 4-5: A = u1 G (per-window tables) and the key's y0 = sqrt(w)
+      // of its parity, for half 0's join; they take part in the join's three
+      // barriers and nothing else
+      gej A;
+      bool ainf;
+      gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
+      fe w, y0, y2, ny;
+      im_load8(im, n_pad, IM_W, i, w.v);
+      fe_sqrt_cand(y0, w);
+      fe_sqr(y2, y0);
+      const bool is_sq = fe_equal(y2, w);
+      fe_normalize(y0);
+      fe_neg(ny, y0);
+      fe_normalize(ny);
+      if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
+        aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
+        aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
+        aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
+      }
+      aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
+      __threadfence_block();
+      __syncthreads();
+      __syncthreads();
+      __syncthreads();
+      continue;
+    }
+#endif
     ge q;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -823,7 +860,7 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_E
     }
 
 #if HKV_YFREE || HKV_SPLIT_YFREE
-    if (SPLIT ? HKV_SPLIT_YFREE : HKV_YFREE) {  // hand B' = (X, Y, Z acc * Zg) on E_w on
+    if (SPLIT ? HKV_SPLIT_YFREE == 1 : HKV_YFREE) {  // hand B' = (X, Y, Z acc * Zg) on E_w on
       if (!SPLIT || half == 0) {                 // (finish kernel / split join kernel)
         fe zt;
         fe_mul(zt, acc.z, Zg);
@@ -843,6 +880,32 @@ __global__ void __launch_bounds__(WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_E
 #endif
     // ---- inversion-free x compare ----
     bool accept = false;
+#if HKV_SPLIT_YFREE == 2
+    if (SPLIT) {  // B = phi^-1(B') = (X, Y, Z acc Zg y0) on E, R = A + B exactly, x compare
+      if (half == 0) {
+        gej A, b;
+        fe y0;
+        uint32_t r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
+          A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
+          A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
+          y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+          r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+        }
+        const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
+        b.x = acc.x;
+        b.y = acc.y;
+        fe zt;
+        fe_mul(zt, acc.z, Zg);
+        fe_mul(b.z, zt, y0);
+        bool rinf = (af & AUXF_AINF) != 0;
+        gej_add_var(A, rinf, b, inf);
+        accept = valid && (af & AUXF_SQ) && !rinf && x_matches_r(A.x, A.z, r);
+      }
+    } else
+#endif
     {
       sc r;
 #pragma unroll
@@ -1671,16 +1734,16 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
 #endif
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
-                         unsigned long long* clk, uint32_t* rare_ctr, hipStream_t st) {
+                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, hipStream_t st) {
   if (split)
-    hipLaunchKernelGGL((hkv_ecmult_kernel<true, HKV_SPLIT_ILP != 0>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab,
-                       qs, bits, n_words, clk, rare_ctr);
+    hipLaunchKernelGGL((hkv_ecmult_kernel<true, HKV_SPLIT_ILP != 0>), dim3(grid), dim3(SPLIT_TPB), 0, st, im, n, n_pad,
+                       gtab, qs, bits, n_words, clk, rare_ctr, aux);
   else if (ilp && HKV_MID_ILP)
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, rare_ctr);
+                       n_words, clk, rare_ctr, aux);
   else
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, rare_ctr);
+                       n_words, clk, rare_ctr, aux);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {

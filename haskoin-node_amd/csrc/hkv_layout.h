@@ -76,15 +76,20 @@ constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF
 // Small batches (the split ecmult) y-free too (HKV_SPLIT_YFREE): the key's
 // square root leaves the prologue's critical path and runs beside the split
 // ecmult (hkv_gsqrt_kernel on an auxiliary stream, with the u1 * G sum);
-// hkv_split_join_kernel maps B' back with y0 and compares. Correct (53/53
-// GPU tests) but off: the auxiliary stream's kernel is not reliably
-// concurrent with the split ecmult (configs[2] block 798 -> 772 us, configs[0]
-// block 754 -> 872 us; profiles/r02_variants_split_yfree.log); running it as
-// extra waves of the split kernel is the way to keep it concurrent.
+// hkv_split_join_kernel maps B' back with y0 and compares. Mode 1 (that aux
+// stream) is correct but its kernel is not reliably concurrent with the split
+// ecmult (configs[2] block 798 -> 772 us, configs[0] block 754 -> 872 us);
+// mode 2 (default) runs the same work as waves 4-5 of the split kernel's own
+// workgroups: configs[0] 755 -> 703 us, configs[2] 796 -> 744 us
+// (profiles/r02_variants_split_yfree.log).
 #ifndef HKV_SPLIT_YFREE
-#define HKV_SPLIT_YFREE 0
+#define HKV_SPLIT_YFREE 2
 #endif
 static_assert(!HKV_SPLIT_YFREE || HKV_YFREE, "the split y-free path uses the y-free helpers and tables");
+// HKV_SPLIT_YFREE=2: the u1 * G sum and the square root run as waves 4-5 of
+// the split kernel's own workgroups (384 threads), so they are concurrent by
+// construction; the join and the compare stay in that kernel.
+constexpr int SPLIT_TPB = HKV_SPLIT_YFREE == 2 ? 384 : 256;
 // hkv_gsqrt_kernel's output (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
 enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_WORDS = 33 };
 constexpr uint32_t AUXF_AINF = 1u, AUXF_SQ = 2u;
