@@ -10,12 +10,14 @@
 //      entries at the default radix 16) on an isomorphic curve (one common Z,
 //      so all Q additions are mixed), then a shared doubling chain of 132
 //      bits with radix-16 Booth digits for k1*Q and k2*(lambda Q).
-//      Split (small-batch) launches also add radix-2^20 Booth digits of
-//      u1_lo*G and u1_hi*(2^128 G) (G entries staged in LDS) and end with the
-//      inversion-free Jacobian x compare (r*Z^2 == X, and (r+n)*Z^2 == X
-//      when r < p-n); verdicts leave as a ballot bitmap. Full-grid launches
-//      are y-free (section 2b): Q is taken on E_w (w = x^3 + 7, no sqrt) and
-//      B' = u2*Q' is handed to
+//      With HKV_SPLIT_YFREE=0, split (small-batch) launches also add
+//      radix-2^20 Booth digits of u1_lo*G and u1_hi*(2^128 G) (G entries
+//      staged in LDS) and end with the inversion-free Jacobian x compare
+//      (r*Z^2 == X, and (r+n)*Z^2 == X when r < p-n); by default (=2) their
+//      waves 4-5 compute u1*G and the key's sqrt beside the Q chains and
+//      half 0 joins exactly; verdicts leave as a ballot bitmap. Full-grid
+//      launches are y-free (section 2b): Q is taken on E_w (w = x^3 + 7, no
+//      sqrt) and B' = u2*Q' is handed to
 //   2b. hkv_finish_kernel, hkv_rare_kernel, hkv_yverdict_kernel — u1*G from
 //      per-window tables, y0 = num/den from "x(u1 G + u2 Q) == r", and the
 //      verdict "y_c^2 == w with the key's parity" (rare lanes: exact sqrt path).
