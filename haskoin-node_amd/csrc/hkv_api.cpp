@@ -160,8 +160,10 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
 #error "y-free: the split ecmult reads y from the one-launch prologue (the three-kernel prologue leaves w)"
 #endif
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
-  HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
-          "prologue launch");
+  // HKV_SPLIT_FUSE: the split ecmult parses the records itself
+  if (!(split && HKV_SPLIT_FUSE))
+    HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
+            "prologue launch");
   const bool split_yf = split && HKV_SPLIT_YFREE == 1;
   if (split && HKV_SPLIT_YFREE && d.aux_n < n_pad) {  // A = u1 G, y0 (hkv_layout.h AUX_*)
     if (d.aux) {
@@ -187,12 +189,12 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
 #define HKV_ILP_ALL 0
 #endif
   const bool ilp = !split && (HKV_ILP_ALL || n_pad <= (size_t)d.grid_max * hkv::WG / 2);
-  const uint32_t blocks = split ? (uint32_t)(n_pad / (hkv::WG / 2))
+  const uint32_t blocks = split ? (uint32_t)(n_pad / hkv::SPLIT_SIGS)
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, ilp ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, ilp,
-                             d.profile ? d.clk : nullptr, d.rare_ctr, d.aux, st),
+                             d.profile ? d.clk : nullptr, d.rare_ctr, d.aux, d_records, mode, st),
           "ecmult launch");
   // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
   // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)

@@ -29,7 +29,8 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
                            hipStream_t st);
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
-                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, hipStream_t st);
+                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, const void* recs,
+                         uint32_t mode, hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 // y-free small batches (HKV_SPLIT_YFREE): u1 * G and y0 beside the split ecmult, then the join
 hipError_t launch_gsqrt(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* aux,

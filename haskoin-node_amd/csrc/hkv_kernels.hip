@@ -373,6 +373,56 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 //     nothing worth batching at this size), u1 = m/s, u2 = r/s, the GLV split
 //     and the Booth recoding. Same intermediate as the three-kernel path.
 // ---------------------------------------------------------------------------
+// The signature half of the split prologue (also waves 4-5 of the fused split
+// ecmult, HKV_SPLIT_FUSE): parse r, s, m, apply the mode's high-S policy,
+// s^-1, u1 = m/s, u2 = r/s, the GLV split and the Booth digits; stores the
+// digits and r for lane i.
+HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_pad, uint32_t mode,
+                      uint32_t* __restrict__ im, uint32_t i, bool& ok, bool& glv_ok, bool& n1, bool& n2) {
+  uint32_t w[24];
+#pragma unroll
+  for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
+  sc r, s, m;
+  rec_be256(r.v, w, 32);
+  rec_be256(s.v, w, 64);
+  rec_be256(m.v, w, 0);
+  ok = (i < n) && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
+  const bool high = sc_is_high(s);
+  if (mode == HKV_MODE_HASKOIN) {
+    sc ns;
+    sc_neg(ns, s);
+    if (high) s = ns;  // secp256k1_ecdsa_signature_normalize
+  } else {
+    ok = ok && !high;  // secp256k1_ecdsa_verify rejects high-S
+  }
+  ok = ok && !u256_is_zero(r.v) && !u256_is_zero(s.v);
+  sc_cond_sub_n(m.v);  // m = msg32 mod n
+  if (!ok) sc_set_u32(s, 1);
+  sc sinv, u1, u2;
+  sc_inv(sinv, s);
+  sc_mul(u1, m, sinv);
+  sc_mul(u2, r, sinv);
+  uint32_t k1[5], k2[5];
+  glv_ok = glv_split(u2, k1, n1, k2, n2);
+  const bool use = ok && glv_ok;
+  uint32_t S1[5], S2[5], SL[4], SH[4];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
+  write_digits(im, n_pad, i, S1, S2, SL, SH);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
+}
+// flags as the three-kernel path leaves them (hkv_glv_kernel)
+HKV_DEV uint32_t split_flags(bool ok, uint32_t pk_ok, bool glv_ok, bool n1, bool n2) {
+  uint32_t f = (ok && (pk_ok & 1u)) ? FLAG_VALID : 0u;
+  f |= pk_ok & (FLAG_YODD | FLAG_COMP);
+  f |= (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
+  if (!glv_ok) f &= ~FLAG_VALID;
+  return f;
+}
+
 __global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* __restrict__ recs, uint32_t n,
                                                                 uint32_t n_pad, uint32_t mode,
                                                                 uint32_t* __restrict__ im) {
@@ -405,51 +455,10 @@ __global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* 
     }
     pk_ok_s[sub] = (pk ? 1u : 0u) | pflags;
   } else {
-    if (i < n) {
-#pragma unroll
-      for (int k = 0; k < 24; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
-    }
-    sc r, s, m;
-    rec_be256(r.v, w, 32);
-    rec_be256(s.v, w, 64);
-    rec_be256(m.v, w, 0);
-    ok = (i < n) && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
-    const bool high = sc_is_high(s);
-    if (mode == HKV_MODE_HASKOIN) {
-      sc ns;
-      sc_neg(ns, s);
-      if (high) s = ns;  // secp256k1_ecdsa_signature_normalize
-    } else {
-      ok = ok && !high;  // secp256k1_ecdsa_verify rejects high-S
-    }
-    ok = ok && !u256_is_zero(r.v) && !u256_is_zero(s.v);
-    sc_cond_sub_n(m.v);  // m = msg32 mod n
-    if (!ok) sc_set_u32(s, 1);
-    sc sinv, u1, u2;
-    sc_inv(sinv, s);
-    sc_mul(u1, m, sinv);
-    sc_mul(u2, r, sinv);
-    uint32_t k1[5], k2[5];
-    glv_ok = glv_split(u2, k1, n1, k2, n2);
-    const bool use = ok && glv_ok;
-    uint32_t S1[5], S2[5], SL[4], SH[4];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
-    write_digits(im, n_pad, i, S1, S2, SL, SH);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
+    sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
   }
   __syncthreads();
-  if (half == 1) {
-    // flags as the three-kernel path leaves them (hkv_glv_kernel)
-    uint32_t f = (ok && (pk_ok_s[sub] & 1u)) ? FLAG_VALID : 0u;
-    f |= pk_ok_s[sub] & (FLAG_YODD | FLAG_COMP);
-    f |= (n1 ? FLAG_NEG1 : 0u) | (n2 ? FLAG_NEG2 : 0u) | (glv_ok ? 0u : FLAG_GLV_OVF);
-    if (!glv_ok) f &= ~FLAG_VALID;
-    im[(size_t)IM_FLAGS * n_pad + i] = f;
-  }
+  if (half == 1) im[(size_t)IM_FLAGS * n_pad + i] = split_flags(ok, pk_ok_s[sub], glv_ok, n1, n2);
 }
 
 // table-entry sign: fe_cneg (XOR + 2-limb fix-up) instead of fe_neg + selects
@@ -542,6 +551,33 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
 HKV_DEV void gej_add_var(gej& acc, bool& inf, const gej& b, bool binf);
 HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]);
 #endif
+#if HKV_SPLIT_YFREE == 2
+// waves 4-5 of the split kernel: A = u1 G and the key's y0 = sqrt(w) of its
+// parity into aux for half 0's join
+HKV_DEV void split_aux_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab,
+                            uint32_t* __restrict__ aux, uint32_t i, bool valid, uint32_t flags, const fe& w) {
+  gej A;
+  bool ainf;
+  gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
+  fe y0, y2, ny;
+  fe_sqrt_cand(y0, w);
+  fe_sqr(y2, y0);
+  const bool is_sq = fe_equal(y2, w);
+  fe_normalize(y0);
+  fe_neg(ny, y0);
+  fe_normalize(ny);
+  if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
+    aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
+    aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
+    aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
+  }
+  aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
+  __threadfence_block();
+}
+#endif
 // HKV_FUSE_FINISH: the full-grid ecmult kernel runs the finish (u1 * G, num,
 // den) itself after storing B', at its own occupancy, instead of a separate
 // hkv_finish_kernel launch. Measured 1-2% slower (the fused kernel spills 168
@@ -560,7 +596,8 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
                                                         uint32_t* __restrict__ bits, uint32_t n_words,
                                                         unsigned long long* __restrict__ clk,
                                                         uint32_t* __restrict__ rare_ctr,
-                                                        uint32_t* __restrict__ aux) {
+                                                        uint32_t* __restrict__ aux,
+                                                        const uint32_t* __restrict__ recs, uint32_t mode) {
   // per wave: two G-entry slots (one in SPLIT mode: a wave adds one G term),
   // each 4 quads x 64 lanes x 16 B (LDS-DMA target); in SPLIT mode reused
   // after the window loop for the half-sum exchange
@@ -570,8 +607,8 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
   __shared__ __attribute__((aligned(16))) uint4 qlds[QLDS ? QLDS_ENTRIES * 4 * WG : 1];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ln = threadIdx.x & 63;
-  constexpr uint32_t PER_WG = SPLIT ? WG / 2 : WG;
-  const int half = SPLIT ? (wv >> 1) : 0;  // wave-uniform
+  constexpr uint32_t PER_WG = SPLIT ? SPLIT_SIGS : WG;
+  const int half = SPLIT ? wv / (SPLIT_SIGS / 64) : 0;  // wave-uniform
   const uint32_t sub = SPLIT ? (threadIdx.x & (PER_WG - 1)) : threadIdx.x;
 
   const uint32_t n_lanes = gridDim.x * WG;
@@ -586,48 +623,73 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
 
   for (uint32_t base = blockIdx.x * PER_WG; base < n_pad; base += gridDim.x * PER_WG) {
     const uint32_t i = base + sub;
-    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-    const bool valid = (i < n) && (flags & FLAG_VALID);
+    uint32_t flags;
+    bool valid;
+    ge q;
+#if HKV_SPLIT_FUSE
+    if (SPLIT) {
+      // fused split prologue: waves 4-5 parse the signature (s^-1, u1, u2,
+      // GLV, digits) while waves 0-3 parse the key and build their tables;
+      // barrier P publishes the digits, r and flags
+      if (half == 2) {
+        bool ok, glv_ok, n1, n2;
+        sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
+        uint32_t kw[REC_WORDS];
+#pragma unroll
+        for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+        fe x, w;
+        uint32_t pflags = 0;
+        const bool pk = pubkey_parse_rec_w(kw, x, w, pflags) && i < n;
+        flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
+        im[(size_t)IM_FLAGS * n_pad + i] = flags;
+        __threadfence_block();
+        __syncthreads();  // barrier P
+        split_aux_lane(im, n_pad, gtab, aux, i, (flags & FLAG_VALID) != 0, flags, w);
+        __syncthreads();
+        __syncthreads();
+        __syncthreads();
+        continue;
+      }
+      uint32_t kw[REC_WORDS];
+#pragma unroll
+      for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+      fe w;
+      uint32_t pflags;
+      const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
+      fe xw, ww;  // Q' = (x w, w^2) on E_w
+      fe_mul(xw, q.x, w);
+      fe_sqr(ww, w);
+      q.x = xw;
+      q.y = ww;
+      if (!pk) ge_set_g(q);  // dummy point (the lane is invalid: its digits are zero)
+    }
+    if (!SPLIT) {
+#else
+    {
+#endif
+    flags = im[(size_t)IM_FLAGS * n_pad + i];
+    valid = (i < n) && (flags & FLAG_VALID);
 #if HKV_SPLIT_YFREE == 2
     if (SPLIT && half == 2) {
       // waves 4-5: A = u1 G (per-window tables) and the key's y0 = sqrt(w)
       // of its parity, for half 0's join; they take part in the join's three
       // barriers and nothing else
-      gej A;
-      bool ainf;
-      gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
-      fe w, y0, y2, ny;
+      fe w;
       im_load8(im, n_pad, IM_W, i, w.v);
-      fe_sqrt_cand(y0, w);
-      fe_sqr(y2, y0);
-      const bool is_sq = fe_equal(y2, w);
-      fe_normalize(y0);
-      fe_neg(ny, y0);
-      fe_normalize(ny);
-      if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
-        aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
-        aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
-        aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
-      }
-      aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
-      __threadfence_block();
+      split_aux_lane(im, n_pad, gtab, aux, i, valid, flags, w);
       __syncthreads();
       __syncthreads();
       __syncthreads();
       continue;
     }
 #endif
-    ge q;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       q.x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
       q.y.v[k] = im[(size_t)(IM_QY + k) * n_pad + i];
     }
 #if HKV_YFREE || HKV_SPLIT_YFREE
-    if (SPLIT ? HKV_SPLIT_YFREE : HKV_YFREE) {  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
+    if (SPLIT ? HKV_SPLIT_YFREE != 0 : HKV_YFREE != 0) {  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
       fe xw, ww;
       fe_mul(xw, q.x, q.y);
       fe_sqr(ww, q.y);
@@ -636,6 +698,14 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
     }
 #endif
     if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
+    }
+#if HKV_SPLIT_FUSE
+    if (SPLIT) {  // barrier P: the signature waves' digits, r and flags are in im
+      __syncthreads();
+      flags = im[(size_t)IM_FLAGS * n_pad + i];
+      valid = (i < n) && (flags & FLAG_VALID);
+    }
+#endif
     const bool neg1 = (flags & FLAG_NEG1) != 0, neg2 = (flags & FLAG_NEG2) != 0;
 
     // ---- table: j*Q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
@@ -1736,16 +1806,18 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
 #endif
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
-                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, hipStream_t st) {
+                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, const void* recs,
+                         uint32_t mode, hipStream_t st) {
+  const uint32_t* rw = (const uint32_t*)recs;
   if (split)
     hipLaunchKernelGGL((hkv_ecmult_kernel<true, HKV_SPLIT_ILP != 0>), dim3(grid), dim3(SPLIT_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, clk, rare_ctr, aux);
+                       gtab, qs, bits, n_words, clk, rare_ctr, aux, rw, mode);
   else if (ilp && HKV_MID_ILP)
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, rare_ctr, aux);
+                       n_words, clk, rare_ctr, aux, rw, mode);
   else
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, rare_ctr, aux);
+                       n_words, clk, rare_ctr, aux, rw, mode);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {

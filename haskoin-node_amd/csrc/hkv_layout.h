@@ -89,7 +89,24 @@ static_assert(!HKV_SPLIT_YFREE || HKV_YFREE, "the split y-free path uses the y-f
 // HKV_SPLIT_YFREE=2: the u1 * G sum and the square root run as waves 4-5 of
 // the split kernel's own workgroups (384 threads), so they are concurrent by
 // construction; the join and the compare stay in that kernel.
-constexpr int SPLIT_TPB = HKV_SPLIT_YFREE == 2 ? 384 : 256;
+// HKV_SPLIT_SIGS: signatures per split workgroup (128: waves 0-1 / 2-3 / 4-5
+// are the halves and the G-sum waves; 64: one wave each, 192 threads)
+#ifndef HKV_SPLIT_SIGS
+#define HKV_SPLIT_SIGS 128
+#endif
+static_assert(HKV_SPLIT_SIGS == 64 || HKV_SPLIT_SIGS == 128, "split workgroups take 64 or 128 signatures");
+constexpr int SPLIT_SIGS = HKV_SPLIT_SIGS;
+constexpr int SPLIT_TPB = (HKV_SPLIT_YFREE == 2 ? 3 : 2) * SPLIT_SIGS;
+// HKV_SPLIT_FUSE: split batches skip hkv_prologue_split_kernel; waves 4-5 of
+// the split ecmult parse the signature (s^-1, u1, u2, GLV, digits) while
+// waves 0-3 parse the key and build their tables, one barrier apart.
+// configs[0] block 701 -> 696 us, configs[2] 743 -> 736 us: the signature
+// half (~65 us of one wave's issue) stays ahead of the chains, only the table
+// build overlaps (profiles/r02_variants_split_fuse.log).
+#ifndef HKV_SPLIT_FUSE
+#define HKV_SPLIT_FUSE 1
+#endif
+static_assert(!HKV_SPLIT_FUSE || HKV_SPLIT_YFREE == 2, "the fused split prologue runs in waves 4-5");
 // hkv_gsqrt_kernel's output (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
 enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_WORDS = 33 };
 constexpr uint32_t AUXF_AINF = 1u, AUXF_SQ = 2u;
