@@ -2,8 +2,9 @@
 //
 // Pipeline per batch (one lane per signature, no MFMA: 256-bit integer work):
 //   1. hkv_prologue_kernel (+ hkv_inv_kernel, hkv_glv_kernel; small batches:
-//      hkv_prologue_split_kernel) — record parse (compact sig + SEC1 pubkey
-//      incl. hybrid keys; the sqrt decompression only on the split path),
+//      inside the split ecmult, HKV_SPLIT_FUSE, or hkv_prologue_split_kernel)
+//      — record parse (compact sig + SEC1 pubkey incl. hybrid keys; the sqrt
+//      decompression only on the classic split path),
 //      high-S policy, m = msg mod n, s^-1, u1 = m/s, u2 = r/s, GLV split of
 //      u2, Booth digits. Writes a SoA intermediate.
 //   2. hkv_ecmult_kernel<SPLIT, ILP> — per-lane table of 1..2^(QW-1) * Q (8
@@ -14,7 +15,8 @@
 //      radix-2^20 Booth digits of u1_lo*G and u1_hi*(2^128 G) (G entries
 //      staged in LDS) and end with the inversion-free Jacobian x compare
 //      (r*Z^2 == X, and (r+n)*Z^2 == X when r < p-n); by default (=2) their
-//      waves 4-5 compute u1*G and the key's sqrt beside the Q chains and
+//      waves 4-5 parse the signature beside the Q tables (HKV_SPLIT_FUSE),
+//      then compute u1*G and the key's sqrt beside the Q chains and
 //      half 0 joins exactly; verdicts leave as a ballot bitmap. Full-grid
 //      launches are y-free (section 2b): Q is taken on E_w (w = x^3 + 7, no
 //      sqrt) and B' = u2*Q' is handed to
