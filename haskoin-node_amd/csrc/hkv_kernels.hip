@@ -273,6 +273,14 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
   }
 }
 
+HKV_DEV void glv_lane(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t flags, const sc& sinv);
+// HKV_INV_GLV: the backward pass runs the GLV step (glv_lane) on each s^-1 as
+// it appears instead of storing it for hkv_glv_kernel. Measured slower (1M
+// batch: 126 + 98 -> 276 us; the serial loop at one wave per SIMD exposes the
+// GLV work's latency; profiles/r02_variants_inv_glv.log), so off.
+#ifndef HKV_INV_GLV
+#define HKV_INV_GLV 0
+#endif
 // (at one wave per SIMD the loop is load-latency bound: each iteration's
 // operands are loaded one iteration ahead)
 __global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t stride, uint32_t* __restrict__ im) {
@@ -330,7 +338,11 @@ __global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t st
       if (k == 0) sc_set_u32(prev, 1);
       sc sinv;
       sc_mul(sinv, inv, prev);
+#if HKV_INV_GLV
+      glv_lane(im, n_pad, i, fl, sinv);
+#else
       im_store8(im, n_pad, IM_C, i, sinv.v);
+#endif
       if (!(fl & FLAG_VALID)) sc_set_u32(sv, 1);
       sc_mul(inv, inv, sv);
       prev = pn;
@@ -341,12 +353,8 @@ __global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t st
 }
 
 // 1c. per signature: u1 = m/s, u2 = r/s, GLV split of u2, Booth digits.
-__global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* __restrict__ im) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n_pad) return;
-  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-  sc sinv, m, r, u1, u2;
-  im_load8(im, n_pad, IM_C, i, sinv.v);
+HKV_DEV void glv_lane(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t flags, const sc& sinv) {
+  sc m, r, u1, u2;
   im_load8(im, n_pad, IM_M, i, m.v);
   im_load8(im, n_pad, IM_R, i, r.v);
   sc_mul(u1, m, sinv);
@@ -364,6 +372,14 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 #pragma unroll
   for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
   write_digits(im, n_pad, i, S1, S2, SL, SH);
+}
+__global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* __restrict__ im) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  sc sinv;
+  im_load8(im, n_pad, IM_C, i, sinv.v);
+  glv_lane(im, n_pad, i, flags, sinv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1799,7 +1815,7 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   stride = stride > 65536u ? stride : (n_pad < 65536u ? n_pad : 65536u);
   hipLaunchKernelGGL(hkv_inv_kernel, dim3(ceil_div(stride, WG)), dim3(WG), 0, st, n_pad, stride, im);
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || HKV_INV_GLV) return e;
   hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
