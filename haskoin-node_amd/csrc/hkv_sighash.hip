@@ -375,6 +375,16 @@ HKV_DEV uint32_t gen_next(Gen& g) {
   return b;
 }
 
+// Block-extraction kernels (hkv_tx_hash_kernel, hkv_sighash_kernel,
+// hkv_std_input_kernel) take one-wave workgroups for up to HKV_XSMALL lanes
+// (a block: its lanes spread over 4x the CUs; configs[0] 696 -> 687 us,
+// configs[2] 736 -> 726 us) and WG-thread ones above (batches of blocks:
+// 64-thread groups measured 1-3% slower there; profiles/r02_variants_xtpb.log).
+// Their LDS slots keep the WG stride either way.
+#ifndef HKV_XSMALL
+#define HKV_XSMALL 16384
+#endif
+static inline uint32_t xtpb_for(size_t n) { return n <= HKV_XSMALL ? 64u : (uint32_t)WG; }
 #ifndef HKV_STREAM_WORDS
 #define HKV_STREAM_WORDS 1
 #endif
@@ -612,7 +622,7 @@ __global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restri
                                                          const uint32_t* __restrict__ tx_off, uint32_t n_tx,
                                                          uint32_t* __restrict__ txt) {
   __shared__ uint32_t buf[16 * WG];
-  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t which = blockIdx.y;  // 0 prevouts, 1 sequences, 2 outputs
   uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (t < n_tx) {
@@ -717,7 +727,7 @@ __global__ void __launch_bounds__(WG) hkv_sighash_kernel(const uint8_t* __restri
                                                          int32_t forkid, uint8_t* __restrict__ out, uint32_t stride,
                                                          uint8_t* __restrict__ status) {
   __shared__ uint32_t buf[16 * WG];
-  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
+  const uint32_t jx = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in_range = jx < n;
   uint32_t stc = HKV_SH_BAD_REF;
   JobCtx c;
@@ -915,7 +925,7 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
                                                            const hkv_input_job* __restrict__ jobs, uint32_t n,
                                                            int32_t forkid, uint8_t* __restrict__ recs) {
   __shared__ uint32_t buf[16 * WG];
-  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
+  const uint32_t jx = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in_range = jx < n;
   bool ok = false;
   const uint32_t* row = txt;
@@ -1566,7 +1576,8 @@ hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t 
                            uint32_t* txt, hipStream_t st) {
   if (n_tx == 0) return hipSuccess;
   if (want_bip143)
-    hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3(blocks_for(n_tx), 3), dim3(WG), 0, st, txs, tx_off, n_tx, txt);
+    hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3((n_tx + xtpb_for(n_tx) - 1) / xtpb_for(n_tx), 3), dim3(xtpb_for(n_tx)), 0, st,
+                       txs, tx_off, n_tx, txt);
   else
     hipLaunchKernelGGL(hkv_tx_index_kernel, dim3(blocks_for(n_tx)), dim3(WG), 0, st, txs, tx_off, n_tx, txt);
   return hipGetLastError();
@@ -1575,7 +1586,7 @@ hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt
                           uint32_t scripts_len, const hkv_sighash_job* jobs, uint32_t n, int32_t forkid, uint8_t* out,
                           uint32_t stride, uint8_t* status, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(hkv_sighash_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts, scripts_len,
+  hipLaunchKernelGGL(hkv_sighash_kernel, dim3((n + xtpb_for(n) - 1) / xtpb_for(n)), dim3(xtpb_for(n)), 0, st, txs, n_tx, txt, scripts, scripts_len,
                      jobs, n, forkid, out, stride, status);
   return hipGetLastError();
 }
@@ -1583,7 +1594,7 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
                              uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                              uint8_t* recs, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(hkv_std_input_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts,
+  hipLaunchKernelGGL(hkv_std_input_kernel, dim3((n + xtpb_for(n) - 1) / xtpb_for(n)), dim3(xtpb_for(n)), 0, st, txs, n_tx, txt, scripts,
                      scripts_len, jobs, n, forkid, recs);
   return hipGetLastError();
 }
