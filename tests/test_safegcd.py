@@ -12,12 +12,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
 
-@pytest.fixture(scope="module")
-def binary(tmp_path_factory):
-    out = str(tmp_path_factory.mktemp("sgcd") / "safegcd_host")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-Wno-unknown-pragmas", "-o", out,
+def build(tmp_path_factory, name, *defs):
+    out = str(tmp_path_factory.mktemp("sgcd") / name)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-Wno-unknown-pragmas", *defs, "-o", out,
                     os.path.join(ROOT, "tests", "safegcd_host.cpp")], check=True)
     return out
+
+
+@pytest.fixture(scope="module")
+def binary(tmp_path_factory):
+    """The default build: the loop stops once g = 0 (HKV_SGCD_EARLY)."""
+    return build(tmp_path_factory, "safegcd_host")
+
+
+@pytest.fixture(scope="module")
+def binary_full(tmp_path_factory):
+    """All 25 iterations (HKV_SGCD_EARLY=0): what a lane that reached g = 0
+    runs on the device while other lanes of its wave still iterate."""
+    return build(tmp_path_factory, "safegcd_host_full", "-DHKV_SGCD_EARLY=0")
 
 
 P = 2**256 - 2**32 - 977
@@ -59,3 +71,14 @@ def test_safegcd_mod_p(binary):
     xs += [P - (rng.getrandbits(rng.randrange(1, 128)) or 1) for _ in range(3000)]
     for x, r in zip(xs, run(binary, xs, "p")):
         assert r == pow(x, -1, P), hex(x)
+
+
+def test_safegcd_full_bound_equals_early_stop(binary, binary_full):
+    """Divsteps after g = 0 are the identity on (f, d) mod the modulus, so the
+    constant-time bound and the early stop give the same inverse."""
+    rng = random.Random(0xE0)
+    xs = [1, 2, 3, N - 1, 2**255, 2**128, 2**30] + [rng.randrange(1, N) for _ in range(5000)]
+    xs += [rng.getrandbits(rng.randrange(1, 64)) or 1 for _ in range(2000)]
+    assert run(binary, xs) == run(binary_full, xs) == [pow(x, -1, N) for x in xs]
+    ps = [1, P - 1] + [rng.randrange(1, P) for _ in range(3000)]
+    assert run(binary, ps, "p") == run(binary_full, ps, "p") == [pow(x, -1, P) for x in ps]
