@@ -3,15 +3,24 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-Workload (BASELINE.json configs[1]): 1,048,576 synthetic valid secp256k1
-(msg32, r, s, pubkey) records PER GPU (weak scaling; at N=8 this is the
-configs[4] IBD shape, 8.4M signatures), generated on device by the keyless
-construction (90% compressed / 10% uncompressed keys from a 65,536-key pool,
-low-S) and resident in HBM before the timed region. One step = the full
-verify of the rank's shard (prologue + ecmult + x-compare -> verdict bitmap)
-plus, for N > 1, the RCCL all-gather of the verdict bitmap (the only
+Workloads (records generated on device by the keyless construction, 90%
+compressed / 10% uncompressed keys from a 65,536-key pool, low-S, resident in
+HBM before the timed region):
+  N = 1 (the headline): BASELINE configs[1], 1,048,576 valid records
+      (seed 0x484B5632); scaling "weak".
+  N > 1 (torchrun), or --config4: BASELINE configs[4], ONE global batch of
+      16,777,216 records (seed 0x484B5635, 5% mutated into rejecting
+      classes), sharded by signature index (hkv/shard.py: contiguous,
+      64-aligned; 2,097,152 per GPU at N = 8). Each rank generates only its
+      slice, records [lo, hi) of that one batch (hkv_gen_batch_device: record
+      k depends on (seed, k) only), with construction labels; scaling
+      "strong" (the total is fixed).
+One step = the verify of the rank's shard (prologue + ecmult + verdict ->
+bitmap) plus, for N > 1, the RCCL all-gather of the verdict bitmap (the only
 collective; hkv/shard.py ShardedVerify). value = all ranks' verifies /
-max-over-ranks time.
+max-over-ranks time. After the timed steps every rank checks its slice of
+the gathered bitmap against its labels and the counts are summed
+(`mismatches`: every bit of the global bitmap against its record's label).
 
 Also reported (rank 0, N = 1): the ecmult stage's roofline (the REFERENCE
 algorithm's limb products per verify, hkv/opcount.py P_ALG_ECMULT, over the
@@ -20,7 +29,8 @@ measured mad rate and clock); configs[0] (the 2,000-tx P2PKH block), [2]
 (block mix) and [3] (adversarial 1M, every class of hkv/adversarial.py); and
 the CPU baseline leg: the C restatement (oracle/, kind "port") and OpenSSL's
 ECDSA_do_verify (the survey's labelled non-reference fallback; libsecp256k1 is
-not installed on the box), single-thread and on the job's CPU share, on the
+not installed on the box), single-thread and over a thread sweep (1, 16, 64,
+128 and the affinity count; the cgroup CPU quota is recorded), on the
 configs[0] block and on config-2 / adversarial samples, with their verdicts
 compared to the GPU's on the same records.
 """
@@ -40,16 +50,44 @@ PER_GPU = 1 << 20
 SEED = 0x484B5632
 POOL = 65536
 UNC_PERMILLE = 100
+# BASELINE configs[4] / SURVEY §8(d) config 5: the IBD-style batch
+CONFIG4_N = 1 << 24
+CONFIG4_SEED = 0x484B5635
+CONFIG4_INVALID_PERMILLE = 50
+
+
+def cgroup_cpu_quota() -> dict:
+    """This job's CPU quota as the kernel enforces it: cgroup v2 cpu.max
+    ("max" or "<quota_us> <period_us>") or v1 cfs_quota_us / cfs_period_us."""
+    out = {}
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us",
+                 "/sys/fs/cgroup/cpu,cpuacct/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                out[path] = f.read().strip()
+        except OSError:
+            continue
+    raw = out.get("/sys/fs/cgroup/cpu.max")
+    if raw:
+        q, _, per = raw.partition(" ")
+        out["quota_cpus"] = None if q == "max" else round(int(q) / int(per or 100000), 2)
+    else:
+        q = out.get("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") or out.get("/sys/fs/cgroup/cpu,cpuacct/cpu.cfs_quota_us")
+        if q is not None:
+            out["quota_cpus"] = None if int(q) < 0 else round(int(q) / 100000, 2)
+    return out
 
 
 def host_info() -> dict:
-    """lscpu model / topology of the box's host and this job's CPU share."""
+    """lscpu model / topology of the box's host and this job's CPU share
+    (affinity mask and cgroup quota)."""
     import subprocess
     info = {"os_cpu_count": os.cpu_count()}
     try:
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         pass
+    info["cgroup"] = cgroup_cpu_quota()
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
@@ -61,14 +99,26 @@ def host_info() -> dict:
     return info
 
 
-def cpu_baseline(samples, threads: int) -> dict:
+def thread_sweep() -> list:
+    """Thread counts of the all-core sweep: 1, 16, 64, 128 and every CPU the
+    affinity mask allows (at most 256, the checkers' pthread cap)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    return sorted({t for t in (1, 16, 64, 128, aff) if t <= max(1, min(aff, 256))} | {min(aff, 256)})
+
+
+def cpu_baseline(samples, sweep) -> dict:
     """The CPU leg (oracle/ is timed here and used as the checker here only).
 
-    samples: [(name, records uint8 [n*168], mode, gpu verdicts bool[n] or None,
-    repeat)]: each implementation verifies the sample on `threads` pthreads
-    (tiled `repeat` times so the run lasts long enough to time; its verdicts
-    on the sample are compared with the GPU's) and its first 4,096 records on
-    one thread.
+    samples: [(name, records uint8 [n*168], mode, gpu verdicts bool[n] or None)].
+    The first sample (configs[0]'s block) is timed at every thread count of
+    `sweep` for each implementation, tiled to 1,500 records per thread (at
+    least the block) so every thread has ~0.15 s of work; `value` is the best
+    rate of the sweep and `cores` the thread count that reached it. The other
+    samples are timed on 1 thread (first 4,096 records) and at that thread
+    count; every sample's verdicts are compared with the GPU's.
     Implementations: "port" = oracle/hkv_oracle.c (C restatement of the
     reference semantics; no GLV, generic inversions), "openssl" = OpenSSL 3
     ECDSA_do_verify behind the semantic adapter (oracle/openssl_check.c) —
@@ -93,30 +143,44 @@ def cpu_baseline(samples, threads: int) -> dict:
         return n / (time.perf_counter() - t0), out.astype(bool)
 
     res = {}
-    for name, recs, mode, gpu, repeat in samples:
+    best = (0.0, "port", 1)  # (rate, impl, threads) on the first sample
+    for si, (name, recs, mode, gpu) in enumerate(samples):
         recs = np.ascontiguousarray(recs)
-        big = np.tile(recs, repeat) if repeat > 1 else recs
-        row = {"records": len(recs) // 168, "mode": "LIBSECP" if mode == 0 else "HASKOIN"}
-        n1 = min(len(recs) // 168, 4096)  # single-thread run: the first 4,096 records
+        n = len(recs) // 168
+        row = {"records": n, "mode": "LIBSECP" if mode == 0 else "HASKOIN"}
+        n1 = min(n, 4096)  # single-thread run: the first 4,096 records
         for iname, fn in impls.items():
             st, _ = run(fn, recs[: n1 * 168], mode, 1)
-            mt, vm = run(fn, big, mode, threads)
-            vm = vm[: len(recs) // 168]
-            row[iname] = {"1_thread": round(st, 1), f"{threads}_threads": round(mt, 1),
-                          "accepts": int(vm.sum())}
+            r = {"1_thread": round(st, 1)}
+            counts = [t for t in sweep if t > 1] if si == 0 else [best[2]] if best[2] > 1 else []
+            vm = None
+            for t in counts:
+                reps = max(1, -(-1500 * t // n))
+                mt, v = run(fn, np.tile(recs, reps) if reps > 1 else recs, mode, t)
+                r[f"{t}_threads"] = round(mt, 1)
+                vm = v[:n] if vm is None else vm
+                if si == 0 and mt > best[0]:
+                    best = (mt, iname, t)
+            if si == 0 and st > best[0]:
+                best = (st, iname, 1)
+            if vm is None:
+                _, vm = run(fn, recs, mode, 1)
+            r["accepts"] = int(vm.sum())
             if gpu is not None:
-                row[iname]["mismatches_vs_gpu"] = int((vm != gpu).sum())
+                r["mismatches_vs_gpu"] = int((vm != gpu).sum())
+            row[iname] = r
         res[name] = row
-    c0 = res.get("config0_block", {})
-    best = max(("port", "openssl"), key=lambda k: c0.get(k, {}).get(f"{threads}_threads", 0.0))
-    return {"value": c0.get(best, {}).get(f"{threads}_threads"), "unit": "verifies/s", "cores": threads,
+    first = samples[0][0] if samples else None
+    rate, impl, cores = best
+    return {"value": round(rate, 1) if first else None, "unit": "verifies/s", "cores": cores,
             "kind": "port",
-            "impl": best,
+            "impl": impl,
             "sample": f"BASELINE configs[0]: the 4,000 inputs of the 2,000-tx P2PKH block (records extracted on "
-                      f"device, HKV_HASKOIN = verifyHashSig), tiled x{threads} for the {threads}-thread run; "
-                      f"the faster of the C restatement (port) and OpenSSL ECDSA_do_verify; libsecp256k1 is "
-                      f"not installed on the box",
-            "single_thread_value": c0.get(best, {}).get("1_thread"),
+                      f"device, HKV_HASKOIN = verifyHashSig), tiled to 1,500 records per thread; best of the C "
+                      f"restatement (port) and OpenSSL ECDSA_do_verify over the thread sweep {list(sweep)} "
+                      f"(value at cores = {cores} threads); libsecp256k1 is not installed on the box",
+            "thread_sweep": list(sweep),
+            "single_thread_value": res.get(first, {}).get(impl, {}).get("1_thread") if first else None,
             "samples": res, "host": host_info()}
 
 
@@ -404,6 +468,10 @@ def main() -> None:
     ap.add_argument("--no-headers", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--config4", action="store_true",
+                    help="BASELINE configs[4] (16,777,216 records, 5%% invalid, seed 0x484B5635, sharded over the "
+                         "ranks); the default whenever WORLD_SIZE > 1")
+    ap.add_argument("--config4-n", type=int, default=CONFIG4_N, help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -425,7 +493,14 @@ def main() -> None:
     from hkv import opcount
     from hkv.shard import ShardedVerify
 
-    n_total = args.per_gpu * world
+    # configs[1] (the N = 1 headline): 1M valid records per GPU, weak scaling.
+    # configs[4] (every N > 1 run, or --config4): ONE global batch of 16M
+    # records (5% invalid) sharded over the ranks, strong scaling.
+    config4 = args.config4 or world > 1
+    if config4:
+        n_total, seed, inv = args.config4_n, CONFIG4_SEED, CONFIG4_INVALID_PERMILLE
+    else:
+        n_total, seed, inv = args.per_gpu * world, SEED, 0
     v = hkv.Verifier(hkv.VerifierConfig(device_ids=[local]))
     # a real (non-null) stream made current: libhkv enqueues on it and the RCCL
     # all-gather, which waits on torch's current stream, is ordered after the
@@ -440,8 +515,11 @@ def main() -> None:
     sv = ShardedVerify(torch, n_total, rank, world, verify_shard, dist=dist)
     n = sv.local_n
     recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
-    # each rank generates exactly its slice of the global synthetic batch
-    v.gen_records_device(0, SEED + sv.lo, n, POOL, UNC_PERMILLE, recs.data_ptr(), sptr)
+    labels = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    # each rank generates exactly records [lo, hi) of the one global batch
+    # (record k depends on (seed, k) only; hkv_gen_batch_device) with their
+    # construction labels
+    v.gen_batch_device(0, seed, sv.lo, n, POOL, UNC_PERMILLE, inv, recs.data_ptr(), labels.data_ptr(), sptr)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -470,12 +548,19 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max, ecm_ms, pro_ms = t.tolist()
 
-    # every constructed signature of the timed batch is valid (construction
-    # labels; the GPU verdicts are compared with CPU implementations on a
-    # sample of these records in the CPU leg below)
+    # self-check of the gathered bitmap: every rank compares its slice of the
+    # assembled global bitmap with its construction labels; the counts are
+    # summed over the ranks (outside the timed region), so every bit of the
+    # gathered bitmap is checked against the label of the same global record
     full = sv.bitmap()
-    accepted = int(np.unpackbits(full.view(np.uint8), bitorder="little")[:n_total].sum())
-    mismatches = n_total - accepted
+    lab_np = labels.cpu().numpy().view(np.uint32)
+    chk = torch.tensor([sv.slice_mismatches(full, lab_np),
+                        int(np.unpackbits(full.view(np.uint8), bitorder="little")[sv.lo:sv.hi].sum()),
+                        int(np.unpackbits(lab_np.view(np.uint8), bitorder="little")[:n].sum())],
+                       dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(chk, op=dist.ReduceOp.SUM)
+    mismatches, accepted, label_valid = chk.tolist()
 
     if rank == 0:
         value = n_total * args.steps / dt_max
@@ -488,36 +573,43 @@ def main() -> None:
         traffic, traffic_raw = load_traffic(args.traffic_json, n)
         c0 = mix = hp = hdr = mkl = adv = None
         c0_recs = c0_got = c0_txs = c0_inputs = adv_recs = adv_got = None
-        if world == 1 and not args.no_config0:
+        single = world == 1 and not config4  # the N = 1 headline run carries the other legs
+        if single and not args.no_config0:
             c0, c0_recs, c0_got, c0_txs, c0_inputs = config0_block(v, torch, args.steps)
-        if world == 1 and not args.no_block_mix:
+        if single and not args.no_block_mix:
             mix = block_mix(v, torch, args.steps)
-        if world == 1 and not args.no_host_path:
+        if single and not args.no_host_path:
             hp = host_path(v, recs, n, args.steps)
-        if world == 1 and not args.no_headers:
+        if single and not args.no_headers:
             hdr = header_batches(v, torch, args.steps)
-        if world == 1 and not args.no_merkle:
+        if single and not args.no_merkle:
             mkl = merkle_batches(v, torch, args.steps)
-        if world == 1 and not args.no_adversarial:
+        if single and not args.no_adversarial:
             adv, adv_recs, adv_got = adversarial_mix(v, torch, n, sptr, args.steps)
         cpu = None
-        if not args.no_cpu_baseline:
-            threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
-                                 else (os.cpu_count() or 1)))
+        if single and not args.no_cpu_baseline:
             samples = []
             if c0_recs is not None:
-                samples.append(("config0_block", c0_recs, 1, c0_got, threads))
+                samples.append(("config0_block", c0_recs, 1, c0_got))
             m2 = min(n, 16384)
             gpu2 = np.unpackbits(full[: (m2 + 31) // 32].view(np.uint8), bitorder="little")[:m2].astype(bool)
-            samples.append(("config1_sample", recs[: m2 * 168].cpu().numpy(), args.mode, gpu2, max(1, threads // 2)))
+            samples.append(("config1_sample", recs[: m2 * 168].cpu().numpy(), args.mode, gpu2))
             if adv_recs is not None:
                 m4 = min(n, 16384)
                 for mode in (0, 1):
                     samples.append((f"config3_sample_{'libsecp' if mode == 0 else 'haskoin'}",
-                                    adv_recs[: m4 * 168], mode, adv_got[mode][:m4], max(1, threads // 2)))
-            cpu = cpu_baseline(samples, threads)
+                                    adv_recs[: m4 * 168], mode, adv_got[mode][:m4]))
+            cpu = cpu_baseline(samples, thread_sweep())
             if c0_recs is not None:
                 cpu["config0_host_sighash"] = cpu_sighash_leg(c0_txs, c0_inputs, c0_recs)
+        if config4:
+            workload = (f"BASELINE configs[4]: one IBD-style batch of {n_total:,} records (configs[1] distribution "
+                        f"plus {inv / 10:g}% invalid: flipped msg32 / r / s bit, another key, the negated key; "
+                        f"seed 0x{seed:X}), contiguous 64-aligned shards, each rank generating only its slice; "
+                        f"one RCCL all-gather of the verdict bitmap per step")
+        else:
+            workload = ("BASELINE configs[1]: 1,048,576 valid (hash,r,s,pubkey) per GPU, 90% compressed / 10% "
+                        "uncompressed keys, 65,536-key pool")
         line = {
             "metric": "ECDSA verifies/sec (1/8 GPU) + verdict mismatches vs libsecp256k1",
             "value": round(value, 1),
@@ -527,18 +619,19 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if config4 else "weak",
             "vs_baseline": None,
             "dtype": "u32 (256-bit integer limbs)",
-            "data": "synthetic (keyless-constructed valid secp256k1 tuples, generated on device)",
-            "config": {"workload": "BASELINE configs[1]: 1,048,576 valid (hash,r,s,pubkey) per GPU, "
-                                   "90% compressed / 10% uncompressed keys, 65,536-key pool; N>1 shards by "
-                                   "signature index + RCCL verdict-bitmap all-gather",
+            "data": "synthetic (keyless-constructed secp256k1 tuples generated on device; labels by construction)",
+            "config": {"workload": workload,
                        "global_batch": n_total, "per_gpu": n, "mode": "LIBSECP" if args.mode == 0 else "HASKOIN",
-                       "parallelism": f"dp{world}"},
+                       "seed": seed, "invalid_permille": inv, "parallelism": f"dp{world}"},
             "mismatches": mismatches,
-            "mismatches_note": "timed batch vs construction labels (all valid); GPU vs CPU implementations on "
-                               "the same records: cpu_baseline.samples.*.*.mismatches_vs_gpu",
+            "accepted": accepted,
+            "label_valid": label_valid,
+            "mismatches_note": "every bit of the (all-gathered) verdict bitmap vs the construction label of the "
+                               "same global record, summed over ranks; GPU vs CPU implementations on the same "
+                               "records: cpu_baseline.samples.*.*.mismatches_vs_gpu (N = 1)",
             "kernel_ms": {"prologue": round(pro_ms, 4), "ecmult": round(ecm_ms, 4)},
             "roofline": {"bound": "valu_int", "achieved": round(achieved, 4), "peak": round(peak, 3),
                          "unit": "T limb-products/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),

@@ -8,8 +8,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -58,7 +60,9 @@ struct DevCtx {
   uint64_t ms_seq = 0;           // last sequence number handed to hkv_ms_scan_kernel
   uint64_t* ms_total_dev = nullptr;  // its device-side address
   void* ms_ctr = nullptr;            // device counters of hkv_ms_scan_kernel
+  bool ms_dirty = false;             // a call failed after its scan launch: zero ms_ctr before the next scan
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
+  bool rare_dirty = false;           // a finish launch failed part-way: zero rare_ctr before the next one
   // split y-free (HKV_SPLIT_YFREE): hkv_gsqrt_kernel's stream, its output and the two ordering events
   hipStream_t aux_stream = nullptr;
   hipEvent_t ev_pro = nullptr, ev_aux = nullptr;
@@ -80,7 +84,14 @@ struct DevCtx {
 
 struct hkv_ctx {
   std::vector<DevCtx> devs;
+  // mu: every entry point's host-side state (DevCtx fields, allocations,
+  // enqueue order). tx_mu[k]: the tx-index rows, the multisig scratch and
+  // the tx staging of device k — held by the sighash / std-input entry
+  // points for their whole call, taken BEFORE mu. hkv_verify_std_inputs_device
+  // releases mu (never tx_mu) while it waits for its multisig count, so the
+  // other entry points keep running on the device meanwhile.
   std::mutex mu;
+  std::vector<std::unique_ptr<std::mutex>> tx_mu;
 };
 struct hkv_batch {
   hkv_ctx* ctx = nullptr;
@@ -101,6 +112,10 @@ int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+// verify-std-inputs batches: the scan kernel sums candidates (<= 136 per
+// 16-of-16 input) in the low 32 bits of one 64-bit device counter
+constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFFFFull / 136;
 
 int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
   if (d.im_cap < n_pad) {
@@ -197,9 +212,21 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
                              d.profile ? d.clk : nullptr, d.rare_ctr, d.aux, d_records, mode, st),
           "ecmult launch");
   // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
-  // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b)
-  if (!split && HKV_YFREE) HKV_TRY(hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st),
-                                   "finish launch");
+  // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b).
+  // The rare-lane count is re-armed by the verdict kernel; a call that failed
+  // between the finish and verdict launches leaves it dirty, so it is zeroed
+  // on the stream first.
+  if (!split && HKV_YFREE) {
+    if (d.rare_dirty) {
+      HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), st), "hipMemset(rare counter)");
+      d.rare_dirty = false;
+    }
+    const hipError_t e = hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st);
+    if (e != hipSuccess) {
+      d.rare_dirty = true;
+      return hip_fail(e, "finish launch");
+    }
+  }
   if (split_yf) {
     HKV_TRY(hipStreamWaitEvent(st, d.ev_aux, 0), "hipStreamWaitEvent(join)");
     HKV_TRY(hkv::launch_split_join(d.im, (uint32_t)n, (uint32_t)n_pad, d.aux, vbits, n_words, st), "join launch");
@@ -312,7 +339,8 @@ int self_check(DevCtx& d) {
   int rc = scratch_acquire(d, d.stream);
   if (!rc) rc = ensure_pool(d, 0x484B5630ull, 16, d.stream);
   if (!rc) {
-    hipError_t e = hkv::launch_gen_records(0x484B5630ull, (uint32_t)n, d.pool, d.pool_n, 250, recs, d.stream);
+    hipError_t e = hkv::launch_gen_records(0x484B5630ull, 0, (uint32_t)n, d.pool, d.pool_n, 250, 0, recs, nullptr,
+                                           d.stream);
     if (e != hipSuccess) rc = hip_fail(e, "selfcheck gen");
   }
   if (!rc) rc = enqueue_verify(d, recs, n, HKV_MODE_LIBSECP, d.stream);
@@ -367,15 +395,43 @@ int enqueue_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, 
   return HKV_OK;
 }
 
+// Wait until hkv_ms_scan_kernel has published sequence number seq (its last
+// workgroup stores the sum, then seq, into the pinned words). Yields on every
+// iteration and sleeps once the wait is long; a launch that failed never
+// publishes, so every 256 iterations the stream's state is checked.
+int wait_ms_total(DevCtx& d, hipStream_t st, uint64_t seq, uint64_t* total) {
+  volatile uint64_t* hv = d.ms_total;
+  for (uint32_t spin = 1; hv[1] != seq; ++spin) {
+    if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else std::this_thread::yield();
+    if ((spin & 255u) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipErrorNotReady) continue;
+      if (hv[1] == seq) break;
+      if (q != hipSuccess) return hip_fail(q, "multisig scan");
+      g_last_hip = "multisig scan finished without publishing its sum";
+      return HKV_E_INTERNAL;
+    }
+  }
+  *total = hv[0];
+  return HKV_OK;
+}
+
 // Full verifyStdInput over a job batch, verdict bit i -> out_bits (device).
 // Single-signature templates: one record per input (recs) through the verify
-// kernels. Multisig (bare / P2SH): the scan kernel's candidate counts are
-// summed on device and read back (the call waits for that 8-byte copy, which
-// runs ahead of the main verify); when there are any, their candidate and
-// key-check records are verified and hkv_ms_resolve_kernel ORs the verdicts
-// of the multisig inputs into out_bits.
+// kernels. Multisig (bare / P2SH / P2WSH): the scan kernel's candidate counts
+// are summed on device and published to a pinned host word; the host reads
+// that sum (the one wait of the device form, overlapped with the main verify
+// already enqueued behind the scan) and, when there are any multisig inputs,
+// enqueues the verify of their candidate and key-check records and
+// hkv_ms_resolve_kernel, which ORs their verdicts into out_bits.
+// lk (the context lock, held by the caller; may be null): released while the
+// host waits for the sum, after publishing this call's scratch use, and
+// re-taken before the multisig work is enqueued (the caller also holds the
+// device's tx lock, which guards txt and the multisig scratch across the gap).
 int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
-                              void* recs, uint32_t* out_bits, hipStream_t st) {
+                              void* recs, uint32_t* out_bits, hipStream_t st,
+                              std::unique_lock<std::mutex>* lk = nullptr) {
   int rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   if (rc) return rc;
   rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
@@ -383,35 +439,35 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   if (rc) return rc;
   uint32_t* desc = static_cast<uint32_t*>(d.ms[0]);
   uint64_t* off = static_cast<uint64_t*>(d.ms[2]);
-  // The scan kernel's last workgroup stores the sum, then the sequence
-  // number, into the pinned words; the host polls them while the main
-  // verify runs (an event record here would put a barrier packet between
-  // the scan and the verify, ~5 us on the block path).
-  volatile uint64_t* hv = d.ms_total;
+  // (an event record here instead of the pinned word would put a barrier
+  // packet between the scan and the verify, ~5 us on the block path)
   const uint64_t seq = ++d.ms_seq;
-  if (n == 0) {  // no launch: publish the empty sum here
-    hv[0] = 0;
-    hv[1] = seq;
+  if (d.ms_dirty) {  // an earlier call failed after its scan launch: counters may be stale
+    HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), st), "hipMemset(multisig counters)");
+    d.ms_dirty = false;
   }
+  d.ms_dirty = true;  // until this call has read the sum
   HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
                               desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq, st),
           "multisig scan launch");
   rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
   if (rc) return rc;
-  for (uint32_t spin = 1; hv[1] != seq; ++spin) {
-    if ((spin & 255u) == 0) {  // a failed launch never publishes: fall back to the stream's state
-      const hipError_t q = hipStreamQuery(st);
-      if (q == hipErrorNotReady) {
-        std::this_thread::yield();
-        continue;
-      }
-      if (hv[1] == seq) break;
-      if (q != hipSuccess) return hip_fail(q, "multisig scan");
-      g_last_hip = "multisig scan finished without publishing its sum";
-      return HKV_E_INTERNAL;
-    }
+  uint64_t total = 0;
+  if (lk) {
+    rc = scratch_release(d, st);
+    if (rc) return rc;
+    lk->unlock();
+    rc = wait_ms_total(d, st, seq, &total);
+    lk->lock();
+    if (rc) return rc;
+    HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+    rc = scratch_acquire(d, st);
+    if (rc) return rc;
+  } else {
+    rc = wait_ms_total(d, st, seq, &total);
+    if (rc) return rc;
   }
-  const uint64_t total = hv[0];
+  d.ms_dirty = false;
   const size_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
   if (n_keys == 0) return HKV_OK;  // no multisig input
   rc = grow(&d.ms[4], &d.ms_cap[4], (n_cand + n_keys) * hkv::REC_SIZE, "hipMalloc(multisig records)");
@@ -486,6 +542,12 @@ int hkv_open_devices(const int* device_ids, int n_ids, uint32_t flags, hkv_ctx**
   hkv_ctx* ctx = new (std::nothrow) hkv_ctx();
   if (!ctx) return HKV_E_OOM;
   ctx->devs.resize(n_ids);
+  for (int k = 0; k < n_ids; ++k) ctx->tx_mu.emplace_back(new (std::nothrow) std::mutex());
+  for (auto& m : ctx->tx_mu)
+    if (!m) {
+      delete ctx;
+      return HKV_E_OOM;
+    }
   for (int k = 0; k < n_ids; ++k) {
     int rc = init_device(ctx->devs[k], device_ids[k]);
     if (!rc && !(flags & HKV_OPEN_NO_SELFCHECK)) rc = self_check(ctx->devs[k]);
@@ -676,10 +738,11 @@ int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, ui
   return scratch_release(d, st);
 }
 
-int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
-                           uint32_t uncompressed_permille, void* d_records, void* hip_stream) {
+int hkv_gen_batch_device(hkv_ctx* ctx, int dev, uint64_t seed, uint64_t index0, size_t n, uint32_t pool_size,
+                         uint32_t uncompressed_permille, uint32_t invalid_permille, void* d_records,
+                         uint32_t* d_labels, void* hip_stream) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !d_records || pool_size == 0 ||
-      uncompressed_permille > 1000 || n > 0xFFFFFF00ull)
+      uncompressed_permille > 1000 || invalid_permille > 1000 || n > 0xFFFFFF00ull || index0 > ~0ull - n)
     return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   std::lock_guard<std::mutex> lock(ctx->mu);
@@ -687,11 +750,20 @@ int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint3
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = scratch_acquire(d, st);
+  // the key pool depends on the batch seed only: every rank of a sharded
+  // batch builds the same pool
   if (!rc) rc = ensure_pool(d, seed ^ 0x706F6F6Cull, pool_size, st);
   if (rc) return rc;
-  HKV_TRY(hkv::launch_gen_records(seed, (uint32_t)n, d.pool, d.pool_n, uncompressed_permille, d_records, st),
+  HKV_TRY(hkv::launch_gen_records(seed, index0, (uint32_t)n, d.pool, d.pool_n, uncompressed_permille,
+                                  invalid_permille, d_records, d_labels, st),
           "gen records launch");
   return scratch_release(d, st);
+}
+
+int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
+                           uint32_t uncompressed_permille, void* d_records, void* hip_stream) {
+  return hkv_gen_batch_device(ctx, dev, seed, 0, n, pool_size, uncompressed_permille, 0, d_records, nullptr,
+                              hip_stream);
 }
 
 int hkv_debug_op(hkv_ctx* ctx, int dev, uint32_t op, size_t n, const uint32_t* d_a, const uint32_t* d_b,
@@ -759,6 +831,7 @@ int hkv_sighash_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_si
     return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   if (!d_jobs || !d_out) return HKV_E_ARG;
+  std::lock_guard<std::mutex> txl(*ctx->tx_mu[dev]);
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
@@ -777,6 +850,7 @@ int hkv_sighash(hkv_ctx* ctx, const hkv_txs* txs, const hkv_sighash_job* jobs, s
   if (!ctx || ctx->devs.empty() || !txs_ok(txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   if (!jobs || !out32) return HKV_E_ARG;
+  std::lock_guard<std::mutex> txl(*ctx->tx_mu[0]);
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[0];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
@@ -803,6 +877,7 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   if (!d_jobs || !d_records) return HKV_E_ARG;
+  std::lock_guard<std::mutex> txl(*ctx->tx_mu[dev]);
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
@@ -815,24 +890,26 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
 
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                                  int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream) {
-  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || n > HKV_MAX_STD_INPUTS) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   if (!d_jobs || !d_records || !d_bits) return HKV_E_ARG;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::mutex> txl(*ctx->tx_mu[dev]);
+  std::unique_lock<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = scratch_acquire(d, st);
-  if (!rc) rc = enqueue_verify_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, d_bits, st);
+  if (!rc) rc = enqueue_verify_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, d_bits, st, &lock);
   if (rc) return rc;
   return scratch_release(d, st);
 }
 
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
                           uint32_t* verdict_bits) {
-  if (!ctx || ctx->devs.empty() || !txs_ok(txs) || n > 0xFFFFFF00ull) return HKV_E_ARG;
+  if (!ctx || ctx->devs.empty() || !txs_ok(txs) || n > HKV_MAX_STD_INPUTS) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   if (!jobs || !verdict_bits) return HKV_E_ARG;
+  std::lock_guard<std::mutex> txl(*ctx->tx_mu[0]);
   std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[0];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");

@@ -41,8 +41,9 @@ hipError_t launch_split_join(const uint32_t* im, uint32_t n, uint32_t n_pad, con
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
-hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,
-                              uint32_t unc_permille, void* recs, hipStream_t st);
+hipError_t launch_gen_records(uint64_t seed, uint64_t index0, uint32_t n, const uint32_t* pool, uint32_t npool,
+                              uint32_t unc_permille, uint32_t invalid_permille, void* recs, uint32_t* labels,
+                              hipStream_t st);
 hipError_t launch_debug(uint32_t op, uint32_t n, const uint32_t* a, const uint32_t* b, uint32_t* out,
                         hipStream_t st);
 hipError_t ecmult_max_blocks_per_cu(int* out);

@@ -1254,7 +1254,9 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
     base = __shfl(base, lead);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rmask >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)rmask, 0u));
-    if (rare) im[(size_t)IM_RARE_LIST * n_pad + base + rank] = i;
+    // (at most n_pad rare lanes per batch; the clamp keeps a stale count from
+    // a failed earlier call inside the row)
+    if (rare && base + rank < n_pad) im[(size_t)IM_RARE_LIST * n_pad + base + rank] = i;
   }
   if (rare) {
     fo |= FLAG_RARE | (ainf ? FLAG_AINF : 0u);
@@ -1290,7 +1292,7 @@ __global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32
 __global__ void __launch_bounds__(WG) hkv_rare_kernel(uint32_t* __restrict__ im, uint32_t n_pad,
                                                       const uint32_t* __restrict__ rare_ctr) {
   const uint32_t k = blockIdx.x * WG + threadIdx.x;
-  if (k >= *rare_ctr) return;
+  if (k >= min(*rare_ctr, n_pad)) return;
   const uint32_t i = im[(size_t)IM_RARE_LIST * n_pad + k];
   const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
   const bool rare = true;
@@ -1617,49 +1619,101 @@ HKV_DEV void put_be256(uint8_t* dst, const uint32_t v[8]) {
 
 // Valid (msg32, r, s, Q) without a secret key: R = aG + bQ, r = R.x mod n,
 // s = r/b, msg = a*s; low-S by s -> n-s (verifies with -R, same x).
-__global__ void __launch_bounds__(WG) hkv_gen_records_kernel(uint64_t seed, uint32_t n,
+// Record i of the launch is record index0 + i of the batch (seed): its random
+// stream depends on the batch index only, so a rank that generates records
+// [lo, hi) with index0 = lo writes exactly that slice of the one global batch
+// (bench.py's configs[4] leg; oracle/hkv_oracle.c hkvo_gen_batch restates it).
+// invalid_permille of the records are then mutated into one of five classes
+// that reject in both modes (GEN_CLS_*); labels (optional, ballot words, bit i
+// = record index0 + i verifies) are the construction labels.
+enum : uint32_t { GEN_CLS_MSG = 0, GEN_CLS_R = 1, GEN_CLS_S = 2, GEN_CLS_KEY = 3, GEN_CLS_NEGKEY = 4, GEN_NCLS = 5 };
+__global__ void __launch_bounds__(WG) hkv_gen_records_kernel(uint64_t seed, uint64_t index0, uint32_t n,
                                                              const uint32_t* __restrict__ pool,
                                                              uint32_t npool, uint32_t unc_permille,
-                                                             uint8_t* __restrict__ recs) {
+                                                             uint32_t invalid_permille,
+                                                             uint8_t* __restrict__ recs,
+                                                             uint32_t* __restrict__ labels) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  uint64_t st = seed * 0xD1B54A32D192ED03ull + (uint64_t)i * 0x9E3779B97F4A7C15ull + 0x8CB92BA72F3D8DD7ull;
-  sc a, b;
-  rand_scalar(a, st);
-  rand_scalar(b, st);
-  const uint64_t pick = splitmix64(st);
-  const uint32_t j = (uint32_t)(pick % npool);
-  const bool unc = ((pick >> 40) % 1000u) < unc_permille;
-  ge q, R;
+  bool label = false;
+  if (i < n) {
+    const uint64_t g = index0 + i;
+    uint64_t st = seed * 0xD1B54A32D192ED03ull + g * 0x9E3779B97F4A7C15ull + 0x8CB92BA72F3D8DD7ull;
+    sc a, b;
+    rand_scalar(a, st);
+    rand_scalar(b, st);
+    const uint64_t pick = splitmix64(st);
+    const uint32_t j = (uint32_t)(pick % npool);
+    const bool unc = ((pick >> 40) % 1000u) < unc_permille;
+    ge q, R;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    q.x.v[k] = pool[(size_t)j * 16 + k];
-    q.y.v[k] = pool[(size_t)j * 16 + 8 + k];
-  }
-  ecmult_simple(R, a, b, q);
-  sc r, s, bi, m;
+    for (int k = 0; k < 8; ++k) {
+      q.x.v[k] = pool[(size_t)j * 16 + k];
+      q.y.v[k] = pool[(size_t)j * 16 + 8 + k];
+    }
+    ecmult_simple(R, a, b, q);
+    sc r, s, bi, m;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) r.v[k] = R.x.v[k];
-  sc_cond_sub_n(r.v);
-  sc_inv(bi, b);
-  sc_mul(s, r, bi);
-  sc_mul(m, a, s);                 // msg = a*s BEFORE the low-S flip:
-  if (sc_is_high(s)) sc_neg(s, s);  // (m, r, -s) verifies with -R (same x)
-  uint8_t* o = recs + (size_t)i * REC_SIZE;
-  put_be256(o, m.v);
-  put_be256(o + 32, r.v);
-  put_be256(o + 64, s.v);
-  o[96] = unc ? 65 : 33;
-  if (unc) {
-    o[97] = 4;
-    put_be256(o + 98, q.x.v);
-    put_be256(o + 130, q.y.v);
-  } else {
-    o[97] = (uint8_t)(2u | (q.y.v[0] & 1u));
-    put_be256(o + 98, q.x.v);
-    for (int k = 130; k < 162; ++k) o[k] = 0;
+    for (int k = 0; k < 8; ++k) r.v[k] = R.x.v[k];
+    sc_cond_sub_n(r.v);
+    sc_inv(bi, b);
+    sc_mul(s, r, bi);
+    sc_mul(m, a, s);                 // msg = a*s BEFORE the low-S flip:
+    if (sc_is_high(s)) sc_neg(s, s);  // (m, r, -s) verifies with -R (same x)
+    // the mutation draw comes after every draw of the valid record, so a
+    // batch with invalid_permille = 0 is the plain generator's batch
+    uint64_t mut = 0;
+    bool bad = false;
+    uint32_t cls = 0, bit = 0;
+    if (invalid_permille) {
+      mut = splitmix64(st);
+      bad = (mut % 1000u) < invalid_permille;
+      cls = (uint32_t)((mut >> 16) % GEN_NCLS);
+      bit = (uint32_t)(mut >> 32) & 255u;
+      if (bad && cls == GEN_CLS_KEY && npool > 1) {  // another key of the pool
+        const uint32_t j2 = (j + 1u + (uint32_t)((mut >> 40) % (npool - 1u))) % npool;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          q.x.v[k] = pool[(size_t)j2 * 16 + k];
+          q.y.v[k] = pool[(size_t)j2 * 16 + 8 + k];
+        }
+      }
+      if (bad && cls == GEN_CLS_KEY && npool <= 1) cls = GEN_CLS_MSG;
+      if (bad && cls == GEN_CLS_NEGKEY) {  // -Q: y -> p - y (compressed keys: the other prefix)
+        fe ny;
+        fe_neg(ny, q.y);
+        fe_normalize(ny);
+        q.y = ny;
+      }
+    }
+    label = !bad;
+    uint8_t* o = recs + (size_t)i * REC_SIZE;
+    put_be256(o, m.v);
+    put_be256(o + 32, r.v);
+    put_be256(o + 64, s.v);
+    o[96] = unc ? 65 : 33;
+    if (unc) {
+      o[97] = 4;
+      put_be256(o + 98, q.x.v);
+      put_be256(o + 130, q.y.v);
+    } else {
+      o[97] = (uint8_t)(2u | (q.y.v[0] & 1u));
+      put_be256(o + 98, q.x.v);
+      for (int k = 130; k < 162; ++k) o[k] = 0;
+    }
+    for (int k = 162; k < REC_SIZE; ++k) o[k] = 0;
+    // a bit of msg32, r or s (big-endian byte bit / 8, bit bit % 8): msg and
+    // r then fail x(R) == r, r or s may overflow n; an s flip cannot land on
+    // n - s, so high-S normalisation (HASKOIN) does not rescue it either
+    if (bad && cls <= GEN_CLS_S) o[32u * cls + (bit >> 3)] ^= (uint8_t)(1u << (bit & 7u));
   }
-  for (int k = 162; k < REC_SIZE; ++k) o[k] = 0;
+  if (labels != nullptr) {
+    const uint64_t ball = __ballot(label);
+    if ((threadIdx.x & 63) == 0 && i < n) {  // ceil(n / 64) * 2 words
+      const uint32_t wi = i / 32;
+      labels[wi] = (uint32_t)ball;
+      labels[wi + 1] = (uint32_t)(ball >> 32);
+    }
+  }
 }
 
 // Block-mix generator hooks (bench.py configs[2], tests): random keys with
@@ -1899,10 +1953,11 @@ hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStr
   hipLaunchKernelGGL(hkv_gen_pool_kernel, dim3(ceil_div(npool, WG)), dim3(WG), 0, st, seed, npool, pool);
   return hipGetLastError();
 }
-hipError_t launch_gen_records(uint64_t seed, uint32_t n, const uint32_t* pool, uint32_t npool,
-                              uint32_t unc_permille, void* recs, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_gen_records_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, seed, n, pool, npool,
-                     unc_permille, (uint8_t*)recs);
+hipError_t launch_gen_records(uint64_t seed, uint64_t index0, uint32_t n, const uint32_t* pool, uint32_t npool,
+                              uint32_t unc_permille, uint32_t invalid_permille, void* recs, uint32_t* labels,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(hkv_gen_records_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, seed, index0, n, pool, npool,
+                     unc_permille, invalid_permille, (uint8_t*)recs, labels);
   return hipGetLastError();
 }
 hipError_t launch_debug(uint32_t op, uint32_t n, const uint32_t* a, const uint32_t* b, uint32_t* out,

@@ -173,9 +173,10 @@ HKV_HD void inv_mod(uint32_t out[8], const uint32_t a[8]) {
     update_fg(f, g, t);
     update_de<M>(d, e, t);
 #if HKV_SGCD_EARLY
-    // g = 0: every further divstep is the identity on (f, d) (matrix
-    // [[2^30, 0], [q, r]] / 2^30), so the loop may stop; on the device when
-    // every lane of the wave has reached it
+    // g = 0: every further divstep leaves f unchanged and d unchanged mod m
+    // (matrix [[2^30, 0], [q, r]] / 2^30; update_de may add m to a negative
+    // d, which the final normalisation folds away), so the loop may stop; on
+    // the device when every lane of the wave has reached it
     const bool gz = (g[0] | g[1] | g[2] | g[3] | g[4] | g[5] | g[6] | g[7] | g[8]) == 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     if (__all(gz)) break;

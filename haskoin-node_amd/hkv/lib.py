@@ -74,7 +74,9 @@ EXPORTS = {
     "hkv_verify_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_uint32, c_void_p, c_void_p]),
     "hkv_gen_records_device": (c_int, [c_void_p, c_int, c_uint64, c_size_t, c_uint32, c_uint32, c_void_p,
                                        c_void_p]),
-    "hkv_sighash": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p, c_void_p]),
+    "hkv_gen_batch_device": (c_int, [c_void_p, c_int, c_uint64, c_uint64, c_size_t, c_uint32, c_uint32, c_uint32,
+                                     c_void_p, c_void_p, c_void_p]),
+    "hkv_sighash":(c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p, c_void_p]),
     "hkv_sighash_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p,
                                    c_size_t, c_void_p, c_void_p]),
     "hkv_std_inputs_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,

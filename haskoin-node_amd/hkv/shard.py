@@ -77,3 +77,14 @@ class ShardedVerify:
         if self.dist is None:
             return self.bits.cpu().numpy().view(np.uint32)[: (self.n + 31) // 32].copy()
         return assemble_bitmap(self.n, self.world, self.gathered.cpu().numpy().view(np.uint32), self.wpr)
+
+    def slice_mismatches(self, full: np.ndarray, labels: np.ndarray) -> int:
+        """Records [lo, hi) of the assembled global bitmap ``full`` against
+        this rank's construction labels (uint32 words, bit 0 = record lo).
+        Summed over ranks this checks every bit of the gathered bitmap."""
+        n = self.hi - self.lo
+        if n == 0:
+            return 0
+        got = np.unpackbits(full.view(np.uint8), bitorder="little")[self.lo:self.hi]
+        want = np.unpackbits(np.ascontiguousarray(labels).view(np.uint8), bitorder="little")[:n]
+        return int((got != want).sum())

@@ -102,6 +102,16 @@ class Verifier:
                                              ctypes.c_void_p(stream_ptr or None))
         check(rc, "hkv_gen_records_device", self.lib)
 
+    def gen_batch_device(self, dev: int, seed: int, index0: int, n: int, pool_size: int, unc_permille: int,
+                         invalid_permille: int, d_records_ptr: int, d_labels_ptr: int = 0,
+                         stream_ptr: int = 0) -> None:
+        """Records [index0, index0 + n) of the synthetic batch `seed`
+        (hkv_gen_batch_device), with construction labels when d_labels_ptr."""
+        rc = self.lib.hkv_gen_batch_device(self.ctx, dev, seed, index0, n, pool_size, unc_permille, invalid_permille,
+                                           ctypes.c_void_p(d_records_ptr), ctypes.c_void_p(d_labels_ptr or None),
+                                           ctypes.c_void_p(stream_ptr or None))
+        check(rc, "hkv_gen_batch_device", self.lib)
+
     # -- signature hashes / standard inputs on device (hkv_*_device) ---------
     def sighash_device(self, dev: int, d_txs, d_jobs: int, n: int, forkid: int, d_out: int, out_stride: int,
                        d_status: int = 0, stream_ptr: int = 0) -> None:

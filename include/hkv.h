@@ -125,6 +125,18 @@ int hkv_verify_device(hkv_ctx* ctx, int dev, const void* d_records, size_t n, ui
  * share of uncompressed keys, all signatures low-S. Enqueued on hip_stream. */
 int hkv_gen_records_device(hkv_ctx* ctx, int dev, uint64_t seed, size_t n, uint32_t pool_size,
                            uint32_t uncompressed_permille, void* d_records, void* hip_stream);
+/* A slice of one synthetic batch: records [index0, index0 + n) of the batch
+ * `seed` (record k depends on (seed, k) only, and the key pool on seed only,
+ * so ranks generating contiguous slices produce exactly the one-process
+ * batch; BASELINE configs[4]). invalid_permille of the records are mutated
+ * into a class that rejects in both modes: a flipped bit of msg32, r or s,
+ * another key of the pool, or the negated key. d_labels (NULL or
+ * ceil(n/64)*2 words): bit i = record index0 + i is valid by construction.
+ * hkv_gen_records_device is this call with index0 = 0, invalid_permille = 0.
+ * CPU restatement (test infrastructure): oracle/hkv_oracle.c hkvo_gen_batch. */
+int hkv_gen_batch_device(hkv_ctx* ctx, int dev, uint64_t seed, uint64_t index0, size_t n, uint32_t pool_size,
+                         uint32_t uncompressed_permille, uint32_t invalid_permille, void* d_records,
+                         uint32_t* d_labels, void* hip_stream);
 
 /* ------------------------------------------------------------------------
  * Signature hashes and standard inputs on device (SURVEY.md §8(a) a7-a9,
@@ -204,11 +216,22 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * every (signature j, key k >= j) pair the walk could compare is verified as
  * its own record, every key of the script is parse-checked, and a resolve
  * kernel replays the walk (count == m and all keys valid). Enqueued on
- * hip_stream; the call itself waits only for the 8-byte count of multisig
- * records (read back ahead of the main verify), not for the verdicts. */
+ * hip_stream; the verdicts are not waited for.
+ * BLOCKING: the call returns only after the multisig scan kernel it enqueues
+ * has EXECUTED on hip_stream (the host needs the batch's multisig record
+ * count to size the multisig work; the main verify is already enqueued
+ * behind the scan while it waits). So hip_stream must be able to make
+ * progress without anything this thread does after the call: a stream
+ * waiting on an event recorded later by the same thread never returns.
+ * While it waits the call holds only this device's sighash / std-input lock
+ * (other threads' calls of the other entry points proceed; their work is
+ * ordered between this call's main verify and its multisig work).
+ * n <= 2^32 / 136 (31,580,641) inputs: a 16-of-16 input yields 136 candidate
+ * records and the batch's candidate sum is a 32-bit device counter. */
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                                  int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream);
-/* Host-memory form of the above; writes ceil(n/32) verdict words. Blocking. */
+/* Host-memory form of the above; writes ceil(n/32) verdict words. Blocking.
+ * Same bound on n. */
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
                           uint32_t* verdict_bits);
 

@@ -28,6 +28,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
+#include <stdlib.h>
 #include <pthread.h>
 
 typedef unsigned __int128 u128;
@@ -398,6 +399,111 @@ int hkvo_verify_batch(const uint8_t* recs, size_t n, int mode, uint8_t* verdicts
   }
   for (int t = 0; t < nthreads; ++t)
     if (created[t]) pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* ---------------- synthetic batch generator (restatement) ----------------
+ * The generator contract of hkv_gen_batch_device (include/hkv.h;
+ * haskoin-node_amd/csrc/hkv_kernels.hip hkv_gen_pool_kernel /
+ * hkv_gen_records_kernel), restated on the CPU so the sharded-batch tests can
+ * build the same records without a GPU: record k of batch `seed` depends on
+ * (seed, k) only, the key pool on seed only. The keyless construction is
+ * R = aG + bQ, r = R.x mod n, s = r/b, msg = a s, s low. */
+static uint64_t splitmix64(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+static void rand_scalar(sc* r, uint64_t* st) {
+  for (int k = 0; k < 4; ++k) r->v[k] = splitmix64(st);
+  if (u256_cmp(r->v, SC_N.v) >= 0) u256_sub(r->v, r->v, SC_N.v);
+  if (u256_is_zero(r->v)) r->v[0] = 1;
+}
+static void u256_to_be(uint8_t* b, const uint64_t* v) {
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 8; ++j) b[(3 - i) * 8 + j] = (uint8_t)(v[i] >> (56 - 8 * j));
+}
+/* a*G + b*P, affine; 0 if infinity */
+static int ecmult_affine(ge* out, const sc* a, const sc* b, const ge* p) {
+  gej R;
+  ecmult(&R, a, b, p);
+  return gej_to_ge(out, &R);
+}
+/* pool key j: d = rand_scalar(seed * C + j * phi + K), Q = d G */
+static void gen_pool(ge* pool, uint64_t seed, uint32_t npool) {
+  static const sc ZERO = {{0, 0, 0, 0}};
+  for (uint32_t j = 0; j < npool; ++j) {
+    uint64_t st = seed * 0x2545F4914F6CDD1DULL + (uint64_t)j * 0x9E3779B97F4A7C15ULL + 0x5851F42D4C957F2DULL;
+    sc d;
+    rand_scalar(&d, &st);
+    ge g = {FE_GX, FE_GY, 0};
+    ecmult_affine(&pool[j], &ZERO, &d, &g);
+  }
+}
+/* mutation classes (hkv_gen_records_kernel GEN_CLS_*): all reject in both modes */
+enum { CLS_MSG = 0, CLS_R = 1, CLS_S = 2, CLS_KEY = 3, CLS_NEGKEY = 4, NCLS = 5 };
+
+/* Records [index0, index0 + n) of batch `seed` into recs (n * 168 bytes);
+ * labels[i] = 1 when record index0 + i is valid by construction (may be
+ * NULL); classes[i] = the mutation class or -1 (may be NULL). The pool
+ * (npool keys) is built from seed ^ "pool" as the device does. */
+int hkvo_gen_batch(uint64_t seed, uint64_t index0, size_t n, uint32_t npool, uint32_t unc_permille,
+                   uint32_t invalid_permille, uint8_t* recs, uint8_t* labels, int8_t* classes) {
+  pthread_once(&g_once, init_g_table);
+  if (npool == 0) return -1;
+  ge* pool = (ge*)calloc(npool, sizeof(ge));
+  if (!pool) return -1;
+  gen_pool(pool, seed ^ 0x706F6F6CULL, npool);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t g = index0 + i;
+    uint64_t st = seed * 0xD1B54A32D192ED03ULL + g * 0x9E3779B97F4A7C15ULL + 0x8CB92BA72F3D8DD7ULL;
+    sc a, b;
+    rand_scalar(&a, &st);
+    rand_scalar(&b, &st);
+    const uint64_t pick = splitmix64(&st);
+    const uint32_t j = (uint32_t)(pick % npool);
+    const int unc = ((pick >> 40) % 1000u) < unc_permille;
+    ge q = pool[j], R;
+    ecmult_affine(&R, &a, &b, &q);
+    sc r, s, bi, m;
+    memcpy(r.v, R.x.v, 32);
+    if (u256_cmp(r.v, SC_N.v) >= 0) u256_sub(r.v, r.v, SC_N.v);
+    sc_inv(&bi, &b);
+    sc_mul(&s, &r, &bi);
+    sc_mul(&m, &a, &s);
+    if (u256_cmp(s.v, SC_HALF_N.v) > 0) u256_sub(s.v, SC_N.v, s.v);
+    int bad = 0, cls = -1;
+    unsigned bit = 0;
+    if (invalid_permille) {
+      const uint64_t mut = splitmix64(&st);
+      bad = (mut % 1000u) < invalid_permille;
+      cls = (int)((mut >> 16) % NCLS);
+      bit = (unsigned)(mut >> 32) & 255u;
+      if (bad && cls == CLS_KEY && npool > 1) q = pool[(j + 1u + (uint32_t)((mut >> 40) % (npool - 1u))) % npool];
+      if (bad && cls == CLS_KEY && npool <= 1) cls = CLS_MSG;
+      if (bad && cls == CLS_NEGKEY) fe_neg(&q.y, &q.y);
+      if (!bad) cls = -1;
+    }
+    uint8_t* o = recs + i * 168;
+    memset(o, 0, 168);
+    u256_to_be(o, m.v);
+    u256_to_be(o + 32, r.v);
+    u256_to_be(o + 64, s.v);
+    o[96] = unc ? 65 : 33;
+    if (unc) {
+      o[97] = 4;
+      u256_to_be(o + 98, q.x.v);
+      u256_to_be(o + 130, q.y.v);
+    } else {
+      o[97] = (uint8_t)(2u | (q.y.v[0] & 1u));
+      u256_to_be(o + 98, q.x.v);
+    }
+    if (bad && cls <= CLS_S) o[32u * (unsigned)cls + (bit >> 3)] ^= (uint8_t)(1u << (bit & 7u));
+    if (labels) labels[i] = (uint8_t)!bad;
+    if (classes) classes[i] = (int8_t)cls;
+  }
+  free(pool);
   return 0;
 }
 

@@ -87,6 +87,24 @@ def host_threads() -> int:
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
 
 
+def c_gen_batch(lib, seed: int, index0: int, n: int, npool: int, unc_permille: int, invalid_permille: int):
+    """Records [index0, index0 + n) of the synthetic batch `seed` from the C
+    restatement of the device generator (oracle/hkv_oracle.c hkvo_gen_batch):
+    (records uint8[n*168], labels bool[n], classes int8[n], -1 = valid)."""
+    import ctypes
+    import numpy as np
+    lib.hkvo_gen_batch.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+    recs = np.zeros(n * 168, dtype=np.uint8)
+    lab = np.zeros(n, dtype=np.uint8)
+    cls = np.zeros(n, dtype=np.int8)
+    rc = lib.hkvo_gen_batch(seed, index0, n, npool, unc_permille, invalid_permille, recs.ctypes.data,
+                            lab.ctypes.data, cls.ctypes.data)
+    assert rc == 0
+    return recs, lab.astype(bool), cls
+
+
 def oracle_batch(lib, recs_bytes: bytes, mode: int, threads: int = 8):
     import ctypes
     import numpy as np

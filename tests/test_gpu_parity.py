@@ -326,32 +326,65 @@ def test_config4_adversarial_1m_both_modes(torch, ver, coracle, openssl):
         assert (got[lo:lo + 262144] == ossl).all(), (mode, "openssl")
 
 
-def test_config5_ibd_16m_sharded_bitmap(torch, ver):
-    """BASELINE configs[4] shape on one GPU: 16,777,216 records (config-2
-    distribution, 5% invalid), verified as the 8 contiguous shards of the
-    8-GPU run (hkv/shard.py) and assembled as the all-gather does; the bitmap
-    equals the single-launch bitmap and the construction labels bit for bit."""
+def gen_batch_dev(torch, ver, seed, index0, n, unc=100, pool=65536, inv=50):
+    d = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
+    lab = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    ver.gen_batch_device(0, seed, index0, n, pool, unc, inv, d.data_ptr(), lab.data_ptr())
+    torch.cuda.synchronize()
+    return d, lab.cpu().numpy().view(np.uint32)
+
+
+def test_gen_batch_matches_c_restatement(torch, ver, coracle):
+    """hkv_gen_batch_device == the C restatement (oracle/hkv_oracle.c
+    hkvo_gen_batch) byte for byte, labels included, at index 0 and at a
+    slice deep inside a 16M batch; invalid_permille = 0 is the plain
+    generator (hkv_gen_records_device)."""
+    from conftest import c_gen_batch
     from hkv import adversarial
-    from hkv.shard import assemble_bitmap, shard_bounds
-    n, world = 1 << 24, 8
-    d = gen_device(torch, ver, n, seed=0x484B5635)
-    twin = gen_twin(torch, ver, d, n, 0x484B5635)
-    adv, lab, _, _ = adversarial.mutate(d.cpu().numpy(), seed=0x484B5635, invalid_frac=0.05, special_frac=0.0,
-                                        twin=twin)
-    del twin
-    d.copy_(torch.from_numpy(adv))
-    del adv
+    for seed, index0, n, pool, inv in ((0x484B5635, 0, 1500, 64, 50), (0x484B5635, 9_999_937, 777, 64, 300),
+                                       (0x484B5632, 123_456, 500, 65536, 0)):
+        d, lab = gen_batch_dev(torch, ver, seed, index0, n, pool=pool, inv=inv)
+        recs, clab, cls = c_gen_batch(coracle, seed, index0, n, pool, 100, inv)
+        got = d.cpu().numpy()
+        bad = np.nonzero((got.reshape(-1, 168) != recs.reshape(-1, 168)).any(axis=1))[0]
+        assert bad.size == 0, (seed, index0, bad[:10], cls[bad[:10]])
+        assert (adversarial.unpack_bits(lab, n) == clab).all()
+    plain = gen_device(torch, ver, 4096, seed=0x484B5632).cpu().numpy()
+    d, lab = gen_batch_dev(torch, ver, 0x484B5632, 0, 4096, inv=0)
+    assert (d.cpu().numpy() == plain).all() and adversarial.unpack_bits(lab, 4096).all()
+
+
+def test_config5_ibd_16m_sharded_bitmap(torch, ver, coracle):
+    """BASELINE configs[4] exactly as bench.py runs it at N = 8, on one GPU:
+    16,777,216 records (seed 0x484B5635, 5% invalid), each of the 8 shards
+    (hkv/shard.py) GENERATED on its own with index0 = lo — as each rank does —
+    and byte-equal to the same slice of the one-launch batch; the shards'
+    verdict words assembled as the all-gather does equal the single-launch
+    bitmap and the construction labels bit for bit; a sample of every shard
+    equals the C restatement's verdicts."""
+    from hkv import adversarial
+    from hkv.shard import assemble_bitmap, shard_bounds, words_per_rank
+    n, world, seed = 1 << 24, 8, 0x484B5635
+    d, lab = gen_batch_dev(torch, ver, seed, 0, n)
+    labels = adversarial.unpack_bits(lab, n)
+    assert 0.045 < 1 - labels.mean() < 0.055
     whole = verify_dev_bits(torch, ver, d, n, 0)[: (n + 31) // 32]
-    wpr = (n // world + 63) // 64 * 2 + 2
+    wpr = words_per_rank(n, world)
     gathered = np.zeros(world * wpr, dtype=np.uint32)
     for r in range(world):
         lo, hi = shard_bounds(n, r, world)
-        w = verify_dev_bits(torch, ver, d, hi - lo, 0, offset=lo)
+        ds, ls = gen_batch_dev(torch, ver, seed, lo, hi - lo)
+        assert torch.equal(ds, d[lo * 168: hi * 168]), r
+        assert (adversarial.unpack_bits(ls, hi - lo) == labels[lo:hi]).all()
+        w = verify_dev_bits(torch, ver, ds, hi - lo, 0)
         gathered[r * wpr: r * wpr + w.size] = w
+        exp = oracle_batch(coracle, ds[:2048 * 168].cpu().numpy().tobytes(), 0, threads=host_threads())
+        assert (adversarial.unpack_bits(w, 2048) == exp).all(), r
+        del ds
     full = assemble_bitmap(n, world, gathered, wpr)
     assert (full == whole).all()
     got = adversarial.unpack_bits(full, n)
-    assert (got == lab).all(), np.nonzero(got != lab)[0][:10]
+    assert (got == labels).all(), np.nonzero(got != labels)[0][:10]
 
 
 def test_split_lane_ecmult_matches_full_grid(torch, ver, coracle):

@@ -60,9 +60,10 @@ def booth(k, w, nwin):
 
 
 def test_booth_recoding_identity():
-    """Radix-32 (Q, hkv_layout.h HKV_QW = 5; radix 16 for HKV_QW = 4) /
-    radix-2^20 (G, GTAB_W) Booth digits as the ecmult kernel extracts them:
-    26 radix-32 windows carry any |k| < 2^129 the GLV split produces."""
+    """Booth digits as the ecmult kernel extracts them: radix 16 (Q windows,
+    the default hkv_layout.h HKV_QW = 4: 33 windows of -8..8), radix 32 (the
+    measured-and-rejected HKV_QW = 5 knob: 26 windows) — each carries any
+    |k| < 2^129 the GLV split produces — and radix 2^20 (G, GTAB_W)."""
     rng = random.Random(9)
     for _ in range(2000):
         k = rng.randrange(2**131)
