@@ -63,11 +63,9 @@ struct DevCtx {
   bool ms_dirty = false;             // a call failed after its scan launch: zero ms_ctr before the next scan
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
   bool rare_dirty = false;           // a finish launch failed part-way: zero rare_ctr before the next one
-  // split y-free (HKV_SPLIT_YFREE): hkv_gsqrt_kernel's stream, its output and the two ordering events
-  hipStream_t aux_stream = nullptr;
-  hipEvent_t ev_pro = nullptr, ev_aux = nullptr;
+  // split launches: waves 4-5's A = u1 G, y0 and flags for the in-kernel join
   uint32_t* aux = nullptr;
-  size_t aux_n = 0;                  // signatures aux holds (the split bound)
+  size_t aux_n = 0;                  // signatures aux holds
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
@@ -113,6 +111,11 @@ int hip_fail(hipError_t e, const char* what) {
 
 size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 
+// split (small-batch) launches when n_pad <= resident grid / HKV_SPLIT_DIV
+#ifndef HKV_SPLIT_DIV
+#define HKV_SPLIT_DIV 8
+#endif
+
 // verify-std-inputs batches: the scan kernel sums candidates (<= 136 per
 // 16-of-16 input) in the low 32 bits of one 64-bit device counter
 constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFFFFull / 136;
@@ -147,8 +150,8 @@ int scratch_release(DevCtx& d, hipStream_t st) {
   return HKV_OK;
 }
 
-// enqueue prologue + ecmult for n records at d_records; verdict words in
-// out_bits ((n + 31) / 32 words, device memory) or, when null, in d.bits
+// enqueue the verify of n records at d_records; verdict words in out_bits
+// ((n + 31) / 32 words, device memory) or, when null, in d.bits
 int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st,
                    uint32_t* out_bits = nullptr) {
   const size_t n_pad = round_up(n, hkv::WG);
@@ -159,77 +162,50 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
     for (auto& x : e) HKV_TRY(hipEventCreate(&x), "hipEventCreate");
     HKV_TRY(hipEventRecord(e[0], st), "hipEventRecord");
   }
-  // a batch of at most half a wave per SIMD (an eighth of the resident grid)
-  // runs two lanes per signature (hkv_ecmult_kernel<true>): a ~24% shorter
-  // dependency chain where latency, not issue, bounds the launch. Above that
-  // the duplicated doublings cost more than the chain saves (measured: a
-  // 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms unsplit). The
-  // same batches run the one-launch prologue (key sqrt beside s^-1 + GLV).
-#ifndef HKV_SPLIT_DIV
-#define HKV_SPLIT_DIV 8  // split when n_pad <= resident grid / HKV_SPLIT_DIV
-#endif
-#ifndef HKV_PROLOGUE_SPLIT
-#define HKV_PROLOGUE_SPLIT 1
-#endif
-#if HKV_YFREE && !HKV_PROLOGUE_SPLIT
-#error "y-free: the split ecmult reads y from the one-launch prologue (the three-kernel prologue leaves w)"
-#endif
+  // A batch of at most half a wave per SIMD (an eighth of the resident grid)
+  // runs the split ecmult (hkv_ecmult_kernel<true>: two lanes per signature
+  // and the G / square-root waves beside them, no separate prologue): a
+  // shorter dependency chain where latency, not issue, bounds the launch.
+  // Above that the duplicated doublings cost more than the chain saves
+  // (measured: a 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms
+  // unsplit; the bound itself re-measured in profiles/r02_split_threshold.log).
   const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
-  // HKV_SPLIT_FUSE: the split ecmult parses the records itself
-  if (!(split && HKV_SPLIT_FUSE))
-    HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, split && HKV_PROLOGUE_SPLIT, st),
-            "prologue launch");
-  const bool split_yf = split && HKV_SPLIT_YFREE == 1;
-  if (split && HKV_SPLIT_YFREE && d.aux_n < n_pad) {  // A = u1 G, y0 (hkv_layout.h AUX_*)
+  if (!split) HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
+  if (split && d.aux_n < n_pad) {  // waves 4-5's A = u1 G and y0 for the join (hkv_layout.h AUX_*)
     if (d.aux) {
-      if (d.aux_stream) HKV_TRY(hipStreamSynchronize(d.aux_stream), "aux sync");
       HKV_TRY(hipStreamSynchronize(st), "aux sync");
       (void)hipFree(d.aux);
       d.aux = nullptr;
+      d.aux_n = 0;
     }
     HKV_TRY(hipMalloc(&d.aux, n_pad * hkv::AUX_WORDS * sizeof(uint32_t)), "hipMalloc(aux)");
     d.aux_n = n_pad;
   }
-  if (split_yf) {  // u1 * G and the key's square root beside the split ecmult (aux stream)
-    HKV_TRY(hipEventRecord(d.ev_pro, st), "hipEventRecord(aux)");
-    HKV_TRY(hipStreamWaitEvent(d.aux_stream, d.ev_pro, 0), "hipStreamWaitEvent(aux)");
-    HKV_TRY(hkv::launch_gsqrt(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.aux, d.aux_stream), "gsqrt launch");
-    HKV_TRY(hipEventRecord(d.ev_aux, d.aux_stream), "hipEventRecord(aux)");
-  }
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
   // instance, every block resident at its 2-wave allocation
-  // (HKV_ILP_ALL: every full-grid batch on the paired-form instance, 2 waves/SIMD)
-#ifndef HKV_ILP_ALL
-#define HKV_ILP_ALL 0
-#endif
-  const bool ilp = !split && (HKV_ILP_ALL || n_pad <= (size_t)d.grid_max * hkv::WG / 2);
+  const bool mid = !split && n_pad <= (size_t)d.grid_max * hkv::WG / 2;
   const uint32_t blocks = split ? (uint32_t)(n_pad / hkv::SPLIT_SIGS)
-                                : (uint32_t)std::min<size_t>(n_pad / hkv::WG, ilp ? d.grid_max / 2 : d.grid_max);
+                                : (uint32_t)std::min<size_t>(n_pad / hkv::WG, mid ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
-  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, ilp,
-                             d.profile ? d.clk : nullptr, d.rare_ctr, d.aux, d_records, mode, st),
+  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, mid,
+                             d.profile ? d.clk : nullptr, d.aux, d_records, mode, st),
           "ecmult launch");
-  // full-grid batches verify y-free (HKV_YFREE): the finish kernels add
-  // u1 * G and decide x(R) == r through y_c = num / den (hkv_kernels.hip §2b).
-  // The rare-lane count is re-armed by the verdict kernel; a call that failed
-  // between the finish and verdict launches leaves it dirty, so it is zeroed
-  // on the stream first.
-  if (!split && HKV_YFREE) {
+  // full-grid batches: the finish kernels add u1 * G and decide x(R) == r
+  // through y_c = num / den (hkv_kernels.hip §2b). The rare-lane count is
+  // re-armed by the verdict kernel; a call that failed between the finish
+  // and verdict launches leaves it dirty, so it is zeroed on the stream first.
+  if (!split) {
     if (d.rare_dirty) {
       HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), st), "hipMemset(rare counter)");
       d.rare_dirty = false;
     }
-    const hipError_t e = hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st);
-    if (e != hipSuccess) {
+    const hipError_t e2 = hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st);
+    if (e2 != hipSuccess) {
       d.rare_dirty = true;
-      return hip_fail(e, "finish launch");
+      return hip_fail(e2, "finish launch");
     }
-  }
-  if (split_yf) {
-    HKV_TRY(hipStreamWaitEvent(st, d.ev_aux, 0), "hipStreamWaitEvent(join)");
-    HKV_TRY(hkv::launch_split_join(d.im, (uint32_t)n, (uint32_t)n_pad, d.aux, vbits, n_words, st), "join launch");
   }
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
@@ -262,16 +238,11 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
   HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
-  if (HKV_SPLIT_YFREE == 1) {  // the split y-free path's auxiliary stream (off by default)
-    HKV_TRY(hipStreamCreateWithFlags(&d.aux_stream, hipStreamNonBlocking), "hipStreamCreate(aux)");
-    HKV_TRY(hipEventCreateWithFlags(&d.ev_pro, hipEventDisableTiming), "hipEventCreate(aux)");
-    HKV_TRY(hipEventCreateWithFlags(&d.ev_aux, hipEventDisableTiming), "hipEventCreate(aux)");
-  }
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
   HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
-  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 448 MiB at radix 2^20 (y-free)
+  HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 448 MiB at radix 2^20
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
   if (per_cu < 1) per_cu = 1;
@@ -309,9 +280,6 @@ void free_device(DevCtx& d) {
   if (d.ms_ctr) (void)hipFree(d.ms_ctr);
   if (d.rare_ctr) (void)hipFree(d.rare_ctr);
   if (d.aux) (void)hipFree(d.aux);
-  if (d.ev_pro) (void)hipEventDestroy(d.ev_pro);
-  if (d.ev_aux) (void)hipEventDestroy(d.ev_aux);
-  if (d.aux_stream) (void)hipStreamDestroy(d.aux_stream);
   if (d.hbits) (void)hipHostFree(d.hbits);
   if (d.clk) (void)hipFree(d.clk);
   if (d.last_use) (void)hipEventDestroy(d.last_use);
@@ -665,11 +633,10 @@ static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_
     // chunk c+1 over PCIe while the verify stream works on chunk c (events
     // order each verify after its own H2D); each chunk's verdict words go to
     // the pinned staging right after its verify, before d.bits is reused.
+    // (one H2D then one verify measured 15.84 ms against 13.09 ms pipelined
+    // for 1M records: profiles/r01_bench_hostpath*.log)
     const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
-#ifndef HKV_PIPELINE_H2D
-#define HKV_PIPELINE_H2D 1  // 0: one H2D then one verify (A/B measurement build)
-#endif
-    const size_t chunk = (HKV_PIPELINE_H2D && len >= 2 * grid_lanes)
+    const size_t chunk = (len >= 2 * grid_lanes)
                              ? grid_lanes * std::max<size_t>(1, (len / 4) / grid_lanes)
                              : len;
     const uint8_t* src = host + shards[k].lo * hkv::REC_SIZE;

@@ -38,19 +38,15 @@ HKV_DEV void gej_cmov(gej& r, const gej& a, bool f) {
   fe_cmov(r.z, a.z, f);
 }
 
-// r = 2a for a = 0 (3M + 4S): A = X^2, B = Y^2, C = B^2, M = X*B (so the
-// usual D = 2((X+B)^2 - A - C) = 4M), E = 3A, F = E^2, X3 = F - 8M,
-// Y3 = E(4M - X3) - 8C, Z3 = 2YZ. On this ISA a product costs about a square,
-// so X*B beats the square-and-subtract form; the power-of-two scalings are
-// funnel shifts. a must not be infinity; y != 0 on secp256k1. r may alias a.
-#ifndef HKV_DBL_HALF
-#define HKV_DBL_HALF 1
-#endif
+// r = 2a for a = 0 (3M + 4S), returned as the same point scaled by 1/2:
+// with A = X^2, B = Y^2, C = B^2, M = X*B, E' = 3A/2,
+//   X3' = E'^2 - 2M, Y3' = E'(M - X3') - C, Z3' = Y*Z,
+// i.e. (X3/4, Y3/8, Z3/2) of the textbook X3 = E^2 - 8M, Y3 = E(4M - X3) - 8C,
+// Z3 = 2YZ: one halving and one shift instead of four power-of-two scalings
+// (-1.4% ecmult, profiles/r02_variants.log). On this ISA a product costs
+// about a square, so X*B beats the square-and-subtract form. a must not be
+// infinity; y != 0 on secp256k1. r may alias a.
 HKV_DEV void gej_double(gej& r, const gej& a) {
-#if HKV_DBL_HALF
-  // The same point scaled by lambda = 1/2, (X3/4, Y3/8, Z3/2): with
-  // E' = 3A/2, Z3' = YZ, X3' = E'^2 - 2M, Y3' = E'(M - X3') - C: one halving
-  // and one shift instead of four shifts.
   fe A, B, C, M, E, t;
   fe_sqr(A, a.x);
   fe_sqr(B, a.y);
@@ -65,24 +61,6 @@ HKV_DEV void gej_double(gej& r, const gej& a) {
   fe_sub(t, M, r.x);
   fe_mul(t, E, t);
   fe_sub(r.y, t, C);        // Y3' = E'(M - X3') - C
-#else
-  fe A, B, C, M, E, t;
-  fe_sqr(A, a.x);
-  fe_sqr(B, a.y);
-  fe_mul(M, a.x, B);
-  fe_sqr(C, B);
-  fe_mul_small(E, A, 3);    // E = 3A
-  fe_mul(r.z, a.y, a.z);
-  fe_shl(r.z, r.z, 1);      // Z3 = 2YZ
-  fe_sqr(t, E);             // F = E^2
-  fe_shl(B, M, 3);          // 8M
-  fe_sub(r.x, t, B);        // X3 = F - 8M
-  fe_shl(M, M, 2);          // D = 4M
-  fe_sub(t, M, r.x);
-  fe_mul(t, E, t);
-  fe_shl(C, C, 3);
-  fe_sub(r.y, t, C);        // Y3 = E(D - X3) - 8C
-#endif
 }
 
 // Mixed addition r = a + (bx, by) where (bx, by) is affine on the curve whose

@@ -25,19 +25,13 @@ enum {
 };
 
 namespace hkv {
-hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im, bool split,
+hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im,
                            hipStream_t st);
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
-                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, const void* recs,
-                         uint32_t mode, hipStream_t st);
+                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool mid,
+                         unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
-// y-free small batches (HKV_SPLIT_YFREE): u1 * G and y0 beside the split ecmult, then the join
-hipError_t launch_gsqrt(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* aux,
-                        hipStream_t st);
-hipError_t launch_split_join(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* aux, uint32_t* bits,
-                             uint32_t n_words, hipStream_t st);
-// y-free full-grid batches (HKV_YFREE): u1 * G, the y0 = num / den reduction and the verdict bitmap
+// y-free full-grid batches: u1 * G, the y0 = num / den reduction and the verdict bitmap
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);

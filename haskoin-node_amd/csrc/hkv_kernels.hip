@@ -1,28 +1,26 @@
 // hkv_kernels.hip — batch secp256k1 ECDSA verify kernels for gfx950.
 //
-// Pipeline per batch (one lane per signature, no MFMA: 256-bit integer work):
-//   1. hkv_prologue_kernel (+ hkv_inv_kernel, hkv_glv_kernel; small batches:
-//      inside the split ecmult, HKV_SPLIT_FUSE, or hkv_prologue_split_kernel)
-//      — record parse (compact sig + SEC1 pubkey incl. hybrid keys; the sqrt
-//      decompression only on the classic split path),
-//      high-S policy, m = msg mod n, s^-1, u1 = m/s, u2 = r/s, GLV split of
-//      u2, Booth digits. Writes a SoA intermediate.
-//   2. hkv_ecmult_kernel<SPLIT, ILP> — per-lane table of 1..2^(QW-1) * Q (8
-//      entries at the default radix 16) on an isomorphic curve (one common Z,
-//      so all Q additions are mixed), then a shared doubling chain of 132
-//      bits with radix-16 Booth digits for k1*Q and k2*(lambda Q).
-//      With HKV_SPLIT_YFREE=0, split (small-batch) launches also add
-//      radix-2^20 Booth digits of u1_lo*G and u1_hi*(2^128 G) (G entries
-//      staged in LDS) and end with the inversion-free Jacobian x compare
-//      (r*Z^2 == X, and (r+n)*Z^2 == X when r < p-n); by default (=2) their
-//      waves 4-5 parse the signature beside the Q tables (HKV_SPLIT_FUSE),
-//      then compute u1*G and the key's sqrt beside the Q chains and
-//      half 0 joins exactly; verdicts leave as a ballot bitmap. Full-grid
-//      launches are y-free (section 2b): Q is taken on E_w (w = x^3 + 7, no
-//      sqrt) and B' = u2*Q' is handed to
+// Pipeline per batch (no MFMA: 256-bit integer work). Every launch shape is
+// y-free: the key's y is never on the critical path (section 2b).
+//   1. hkv_prologue_kernel + hkv_inv_kernel + hkv_glv_kernel (full-grid
+//      batches) — record parse (compact sig + SEC1 pubkey incl. hybrid keys,
+//      w = x^3 + 7 instead of the sqrt), high-S policy, m = msg mod n, s^-1
+//      (batched), u1 = m/s, u2 = r/s, GLV split of u2, Booth digits. Writes a
+//      SoA intermediate.
+//   2. hkv_ecmult_kernel<SPLIT, ILP> — per-lane table of 1..2^(QW-1) * Q' (8
+//      entries at the default radix 16) on an isomorphic curve of E_w (one
+//      common Z, so all Q additions are mixed), then a shared doubling chain
+//      of 132 bits with radix-16 Booth digits for k1*Q' and k2*(lambda Q').
+//      Full-grid launches (SPLIT = false; ILP = the paired-form instance for
+//      mid-size batches) leave B' = u2*Q' to
 //   2b. hkv_finish_kernel, hkv_rare_kernel, hkv_yverdict_kernel — u1*G from
 //      per-window tables, y0 = num/den from "x(u1 G + u2 Q) == r", and the
 //      verdict "y_c^2 == w with the key's parity" (rare lanes: exact sqrt path).
+//      Split launches (small batches, SPLIT = true): waves 4-5 of each
+//      workgroup parse the signature beside the Q tables, then compute u1*G
+//      and the key's sqrt beside the two Q chains (waves 0-1: k1, 2-3: k2),
+//      and half 0 joins exactly (R = A + B, Jacobian x compare); verdicts
+//      leave as a ballot bitmap.
 //   3. hkv_gtable_kernel    — once per context: the fixed-base tables.
 //   4. hkv_gen_*            — synthetic valid batches (keyless construction,
 //      SURVEY.md §8(c)) for the benchmark and the tests.
@@ -106,7 +104,7 @@ HKV_DEV bool pubkey_parse_rec(const uint32_t* w, fe& x, fe& y) {
   }
   return pk_ok;
 }
-// The y-free form of the parse (HKV_YFREE): the same accept rules except the
+// The y-free form of the parse: the same accept rules except the
 // one that needs the square root — x^3 + 7 of a compressed key is not shown
 // to be a square here; the finish kernels' y_c^2 == w test rejects a
 // non-square (no y_c exists), and their rare paths test it explicitly.
@@ -177,11 +175,7 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(co
   // --- pubkey: secp256k1_ec_pubkey_parse (y-free: y stays implicit, IM_QY = w)
   fe x, y;
   uint32_t pflags = 0;
-#if HKV_YFREE
   ok = pubkey_parse_rec_w(w, x, y, pflags) && ok;
-#else
-  ok = pubkey_parse_rec(w, x, y) && ok;
-#endif
 
   const uint32_t flags = (ok ? FLAG_VALID : 0u) | pflags;
   im[(size_t)IM_FLAGS * n_pad + i] = flags;
@@ -273,14 +267,6 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
   }
 }
 
-HKV_DEV void glv_lane(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t flags, const sc& sinv);
-// HKV_INV_GLV: the backward pass runs the GLV step (glv_lane) on each s^-1 as
-// it appears instead of storing it for hkv_glv_kernel. Measured slower (1M
-// batch: 126 + 98 -> 276 us; the serial loop at one wave per SIMD exposes the
-// GLV work's latency; profiles/r02_variants_inv_glv.log), so off.
-#ifndef HKV_INV_GLV
-#define HKV_INV_GLV 0
-#endif
 // (at one wave per SIMD the loop is load-latency bound: each iteration's
 // operands are loaded one iteration ahead)
 __global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t stride, uint32_t* __restrict__ im) {
@@ -338,11 +324,7 @@ __global__ void __launch_bounds__(WG) hkv_inv_kernel(uint32_t n_pad, uint32_t st
       if (k == 0) sc_set_u32(prev, 1);
       sc sinv;
       sc_mul(sinv, inv, prev);
-#if HKV_INV_GLV
-      glv_lane(im, n_pad, i, fl, sinv);
-#else
       im_store8(im, n_pad, IM_C, i, sinv.v);
-#endif
       if (!(fl & FLAG_VALID)) sc_set_u32(sv, 1);
       sc_mul(inv, inv, sv);
       prev = pn;
@@ -383,16 +365,13 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 }
 
 // ---------------------------------------------------------------------------
-// 1d. small batches (the split ecmult's range, e.g. one block): prologue,
-//     s^-1 and GLV in one launch, the two independent dependency chains side
-//     by side instead of three consecutive kernels. A workgroup takes 128
-//     signatures: waves 0-1 parse the key (the 253S + 13M sqrt), waves 2-3
-//     parse the signature and run s^-1 (safegcd, one per signature: there is
-//     nothing worth batching at this size), u1 = m/s, u2 = r/s, the GLV split
-//     and the Booth recoding. Same intermediate as the three-kernel path.
+// 1d. small batches (the split ecmult's range, e.g. one block): no separate
+//     prologue launch; waves 4-5 of each split-ecmult workgroup parse the
+//     signatures (below) while waves 0-3 parse the keys and build their
+//     Q tables.
 // ---------------------------------------------------------------------------
-// The signature half of the split prologue (also waves 4-5 of the fused split
-// ecmult, HKV_SPLIT_FUSE): parse r, s, m, apply the mode's high-S policy,
+// The signature half of a split workgroup (waves 4-5): parse r, s, m, apply
+// the mode's high-S policy,
 // s^-1, u1 = m/s, u2 = r/s, the GLV split and the Booth digits; stores the
 // digits and r for lane i.
 HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_pad, uint32_t mode,
@@ -432,7 +411,7 @@ HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_
 #pragma unroll
   for (int k = 0; k < 8; ++k) im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
 }
-// flags as the three-kernel path leaves them (hkv_glv_kernel)
+// flags as the full-grid kernels leave them (hkv_glv_kernel)
 HKV_DEV uint32_t split_flags(bool ok, uint32_t pk_ok, bool glv_ok, bool n1, bool n2) {
   uint32_t f = (ok && (pk_ok & 1u)) ? FLAG_VALID : 0u;
   f |= pk_ok & (FLAG_YODD | FLAG_COMP);
@@ -441,48 +420,6 @@ HKV_DEV uint32_t split_flags(bool ok, uint32_t pk_ok, bool glv_ok, bool n1, bool
   return f;
 }
 
-__global__ void __launch_bounds__(WG) hkv_prologue_split_kernel(const uint32_t* __restrict__ recs, uint32_t n,
-                                                                uint32_t n_pad, uint32_t mode,
-                                                                uint32_t* __restrict__ im) {
-  __shared__ uint32_t pk_ok_s[WG / 2];
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int half = wv >> 1;  // wave-uniform
-  const uint32_t sub = threadIdx.x & (WG / 2 - 1);
-  const uint32_t i = blockIdx.x * (WG / 2) + sub;  // < n_pad (n_pad % WG == 0)
-  uint32_t w[REC_WORDS];
-#pragma unroll
-  for (int k = 0; k < REC_WORDS; ++k) w[k] = 0;
-  bool ok = false, glv_ok = false, n1 = false, n2 = false;
-  if (half == 0) {
-    if (i < n) {
-#pragma unroll
-      for (int k = 24; k < 42; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
-    }
-    fe x, y;
-#if HKV_SPLIT_YFREE
-    uint32_t pflags = 0;  // y stays implicit: IM_QY = w (the square root runs beside the ecmult)
-    const bool pk = pubkey_parse_rec_w(w, x, y, pflags) && i < n;
-#else
-    const uint32_t pflags = 0;
-    const bool pk = pubkey_parse_rec(w, x, y) && i < n;
-#endif
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      im[(size_t)(IM_QX + k) * n_pad + i] = x.v[k];
-      im[(size_t)(IM_QY + k) * n_pad + i] = y.v[k];
-    }
-    pk_ok_s[sub] = (pk ? 1u : 0u) | pflags;
-  } else {
-    sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
-  }
-  __syncthreads();
-  if (half == 1) im[(size_t)IM_FLAGS * n_pad + i] = split_flags(ok, pk_ok_s[sub], glv_ok, n1, n2);
-}
-
-// table-entry sign: fe_cneg (XOR + 2-limb fix-up) instead of fe_neg + selects
-#ifndef HKV_CNEG
-#define HKV_CNEG 1
-#endif
 // ---------------------------------------------------------------------------
 // 2. ecmult + x compare
 // ---------------------------------------------------------------------------
@@ -510,16 +447,14 @@ HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32
 // four uint4 quads at [j][quad][thread] (a wave's 64 lanes read 1 KB
 // contiguous per quad). 8 entries x 64 B x 256 threads = 128 KB; with
 // < 1 wave per SIMD the LDS latency replaces an L2 round trip per lookup.
-// HKV_SPLIT_QLDS=0 keeps the table in scratch as the full-grid kernel does.
+// (A 16-entry radix-32 table, HKV_QW = 5, does not fit: it stays in scratch
+// as the full-grid kernel's does.)
 // SPLIT launches run < 1 wave per SIMD, so they take the whole register
 // file (196 VGPRs, no spill) instead of the full grid's 4-wave budget.
 #ifndef HKV_SPLIT_WAVES
 #define HKV_SPLIT_WAVES 1
 #endif
-#ifndef HKV_SPLIT_QLDS
-#define HKV_SPLIT_QLDS 1
-#endif
-constexpr int QLDS_ENTRIES = (HKV_SPLIT_QLDS && QTAB_ENTRIES <= 8) ? QTAB_ENTRIES : 0;
+constexpr int QLDS_ENTRIES = QTAB_ENTRIES <= 8 ? QTAB_ENTRIES : 0;
 HKV_DEV void qlds_store(uint4* t, int entry, const fe& x, const fe& y) {
   uint4* p = t + (size_t)entry * 4 * WG + threadIdx.x;
   p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
@@ -537,19 +472,14 @@ HKV_DEV void qlds_load(const uint4* t, int entry, fe& x, fe& y) {
 }
 
 // SPLIT (small batches, when one lane per signature would leave the GPU
-// half empty): a workgroup takes 128 signatures; waves 0-1 run the k1*Q and
-// u1_lo*G half of the sum, waves 2-3 the k2*(lambda Q) and u1_hi*(2^128 G)
-// half, each with its own doubling chain (the slot loops become wave-
-// uniform, so each wave issues half the additions), and the halves meet in
-// LDS for one Jacobian addition before the x compare. The per-signature
-// dependency chain shrinks by about a quarter; total work grows by the
-// duplicated doublings and table, so large batches use SPLIT = false.
-// SPLIT launches use the paired-product group forms (HKV_SPLIT_ILP=0: the
-// plain ones); the full grid keeps the plain forms, its 4 waves per SIMD
-// already fill the issue slots.
-#ifndef HKV_SPLIT_ILP
-#define HKV_SPLIT_ILP 1
-#endif
+// half empty): a workgroup takes 128 signatures; waves 0-1 run k1*Q', waves
+// 2-3 k2*(lambda Q'), each with its own doubling chain (the slot loops become
+// wave-uniform, so each wave issues half the additions), and the halves meet
+// in LDS for one Jacobian addition. The per-signature dependency chain
+// shrinks by about a quarter; total work grows by the duplicated doublings
+// and table, so large batches use SPLIT = false. SPLIT launches use the
+// paired-product group forms; the full grid keeps the plain forms (its 4
+// waves per SIMD already fill the issue slots) except for mid-size batches.
 template <bool ILP>
 HKV_DEV void ec_double(gej& acc) {
   if constexpr (ILP) gej_double_ilp(acc, acc);
@@ -561,15 +491,10 @@ HKV_DEV void ec_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, cons
   else gej_accumulate(acc, inf, az, tx, ty, take);
 }
 
-#if HKV_YFREE
-HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
-                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags);
 HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab, uint32_t i,
                        bool valid, gej& A, bool& ainf);
 HKV_DEV void gej_add_var(gej& acc, bool& inf, const gej& b, bool binf);
 HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]);
-#endif
-#if HKV_SPLIT_YFREE == 2
 // waves 4-5 of the split kernel: A = u1 G and the key's y0 = sqrt(w) of its
 // parity into aux for half 0's join
 HKV_DEV void split_aux_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab,
@@ -595,14 +520,6 @@ HKV_DEV void split_aux_lane(const uint32_t* __restrict__ im, uint32_t n_pad, con
   aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
   __threadfence_block();
 }
-#endif
-// HKV_FUSE_FINISH: the full-grid ecmult kernel runs the finish (u1 * G, num,
-// den) itself after storing B', at its own occupancy, instead of a separate
-// hkv_finish_kernel launch. Measured 1-2% slower (the fused kernel spills 168
-// VGPRs at 4 waves per SIMD; profiles/r02_variants_fuse.log), so off.
-#ifndef HKV_FUSE_FINISH
-#define HKV_FUSE_FINISH 0
-#endif
 // ILP: the paired-product group forms. The split kernel uses them (< 1 wave
 // per SIMD); full-grid launches of mid-size batches (at most 2 waves per
 // SIMD: 32k-131k signatures) take the <false, true> instance, which is
@@ -613,18 +530,13 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
                                                         uint32_t* __restrict__ qs,
                                                         uint32_t* __restrict__ bits, uint32_t n_words,
                                                         unsigned long long* __restrict__ clk,
-                                                        uint32_t* __restrict__ rare_ctr,
                                                         uint32_t* __restrict__ aux,
                                                         const uint32_t* __restrict__ recs, uint32_t mode) {
-  // per wave: two G-entry slots (one in SPLIT mode: a wave adds one G term),
-  // each 4 quads x 64 lanes x 16 B (LDS-DMA target); in SPLIT mode reused
-  // after the window loop for the half-sum exchange
-  constexpr int GSLOTS = SPLIT ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) uint4 gpf[WG / 64][GSLOTS][4][64];
+  // SPLIT: half 1 hands (X, Y, Z, inf) to half 0 through LDS, word-major [25][SPLIT_SIGS]
+  __shared__ uint32_t xch[SPLIT ? 25 * SPLIT_SIGS : 1];
   constexpr bool QLDS = SPLIT && QLDS_ENTRIES > 0;
   __shared__ __attribute__((aligned(16))) uint4 qlds[QLDS ? QLDS_ENTRIES * 4 * WG : 1];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ln = threadIdx.x & 63;
   constexpr uint32_t PER_WG = SPLIT ? SPLIT_SIGS : WG;
   const int half = SPLIT ? wv / (SPLIT_SIGS / 64) : 0;  // wave-uniform
   const uint32_t sub = SPLIT ? (threadIdx.x & (PER_WG - 1)) : threadIdx.x;
@@ -644,11 +556,12 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
     uint32_t flags;
     bool valid;
     ge q;
-#if HKV_SPLIT_FUSE
     if (SPLIT) {
-      // fused split prologue: waves 4-5 parse the signature (s^-1, u1, u2,
-      // GLV, digits) while waves 0-3 parse the key and build their tables;
-      // barrier P publishes the digits, r and flags
+      // waves 4-5 parse the signature (s^-1, u1, u2, GLV, digits) while
+      // waves 0-3 parse the key and build their tables; barrier P publishes
+      // the digits, r and flags; then waves 4-5 compute A = u1 G and the
+      // key's y0 = sqrt(w) for half 0's join, taking part in the join's
+      // two barriers and nothing else
       if (half == 2) {
         bool ok, glv_ok, n1, n2;
         sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
@@ -663,9 +576,8 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
         __threadfence_block();
         __syncthreads();  // barrier P
         split_aux_lane(im, n_pad, gtab, aux, i, (flags & FLAG_VALID) != 0, flags, w);
-        __syncthreads();
-        __syncthreads();
-        __syncthreads();
+        __syncthreads();  // barrier A: aux and half 1's sum are published
+        __syncthreads();  // barrier B: half 0 has read them
         continue;
       }
       uint32_t kw[REC_WORDS];
@@ -680,53 +592,25 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
       q.x = xw;
       q.y = ww;
       if (!pk) ge_set_g(q);  // dummy point (the lane is invalid: its digits are zero)
-    }
-    if (!SPLIT) {
-#else
-    {
-#endif
-    flags = im[(size_t)IM_FLAGS * n_pad + i];
-    valid = (i < n) && (flags & FLAG_VALID);
-#if HKV_SPLIT_YFREE == 2
-    if (SPLIT && half == 2) {
-      // waves 4-5: A = u1 G (per-window tables) and the key's y0 = sqrt(w)
-      // of its parity, for half 0's join; they take part in the join's three
-      // barriers and nothing else
-      fe w;
-      im_load8(im, n_pad, IM_W, i, w.v);
-      split_aux_lane(im, n_pad, gtab, aux, i, valid, flags, w);
-      __syncthreads();
-      __syncthreads();
-      __syncthreads();
-      continue;
-    }
-#endif
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      q.x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
-      q.y.v[k] = im[(size_t)(IM_QY + k) * n_pad + i];
-    }
-#if HKV_YFREE || HKV_SPLIT_YFREE
-    if (SPLIT ? HKV_SPLIT_YFREE != 0 : HKV_YFREE != 0) {  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
-      fe xw, ww;
-      fe_mul(xw, q.x, q.y);
-      fe_sqr(ww, q.y);
-      q.x = xw;
-      q.y = ww;
-    }
-#endif
-    if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
-    }
-#if HKV_SPLIT_FUSE
-    if (SPLIT) {  // barrier P: the signature waves' digits, r and flags are in im
-      __syncthreads();
+      __syncthreads();  // barrier P: the signature waves' digits, r and flags are in im
       flags = im[(size_t)IM_FLAGS * n_pad + i];
       valid = (i < n) && (flags & FLAG_VALID);
+    } else {
+      flags = im[(size_t)IM_FLAGS * n_pad + i];
+      valid = (i < n) && (flags & FLAG_VALID);
+      fe x, w;  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        x.v[k] = im[(size_t)(IM_QX + k) * n_pad + i];
+        w.v[k] = im[(size_t)(IM_W + k) * n_pad + i];
+      }
+      fe_mul(q.x, x, w);
+      fe_sqr(q.y, w);
+      if (!valid) ge_set_g(q);  // dummy point; all digits are zero for this lane
     }
-#endif
     const bool neg1 = (flags & FLAG_NEG1) != 0, neg2 = (flags & FLAG_NEG2) != 0;
 
-    // ---- table: j*Q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
+    // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
     // Pass 1 streams raw entries to the lane's scratch (z-ratios H_j parked in
     // the beta*x slot of entry j-1); pass 2 walks back rescaling every entry
     // to the common Z (rho_j = prod_{k>j} H_k) and writes beta*x (SPLIT mode:
@@ -795,8 +679,7 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
     }
 
     // ---- shared doubling chain, 33 radix-16 windows ----
-    // Window w's digit word and the two Q-table entries it selects are
-    // loaded before the window's four doublings, hiding their latency.
+    // Window w's digit word is loaded one window ahead, hiding its latency.
     gej acc;
     bool inf = true;
     fe_set_zero(acc.x);
@@ -809,33 +692,13 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
       const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
       const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
-      // y-free full-grid launches leave u1 * G to the finish kernel
-      const bool gwin = (SPLIT ? !HKV_SPLIT_YFREE : !HKV_YFREE) && (win % GSTEP) == 0;
-      uint32_t gd0 = 0, gd1 = 0;
-      if (gwin) {
-        const int gj = win / GSTEP;
-        gd0 = valid ? im[(size_t)(IM_GDIG + 2 * gj) * n_pad + i] : 0u;
-        gd1 = valid ? im[(size_t)(IM_GDIG + 2 * gj + 1) * n_pad + i] : 0u;
-        const uint32_t m0 = gd0 & GD_MAG, m1 = gd1 & GD_MAG;
-        const uint4* e0 = reinterpret_cast<const uint4*>(gtab) + (size_t)(m0 ? m0 - 1 : 0) * 4;
-        const uint4* e1 = reinterpret_cast<const uint4*>(gtab) + ((size_t)GTAB_ENTRIES + (m1 ? m1 - 1 : 0)) * 4;
-#pragma unroll
-        for (int qd = 0; qd < 4; ++qd) {
-          if (SPLIT) {  // one G term per wave
-            __builtin_amdgcn_global_load_lds((half ? e1 : e0) + qd, (__attribute__((address_space(3))) void*)&gpf[wv][0][qd][0], 16, 0, 0);
-          } else {
-            __builtin_amdgcn_global_load_lds(e0 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][0][qd][0], 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(e1 + qd, (__attribute__((address_space(3))) void*)&gpf[wv][GSLOTS - 1][qd][0], 16, 0, 0);
-          }
-        }
-      }
       if (win != NWIN - 1) {
 #pragma unroll 1
         for (int d = 0; d < QW; ++d) {
           if (!inf) ec_double<ILP>(acc);
         }
       }
-      // Q terms: slot 0 = k1 * Q, slot 1 = k2 * lambda(Q)
+      // Q terms: slot 0 = k1 * Q', slot 1 = k2 * lambda(Q')
 #pragma unroll 1
       for (int slot = 0; slot < 2; ++slot) {
         if (SPLIT && slot != half) continue;
@@ -849,177 +712,77 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
           qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
           qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
         }
-#if HKV_CNEG
         fe_cneg(ty, ty, neg);
-#else
-        fe nty;
-        fe_neg(nty, ty);
-        fe_cmov(ty, nty, neg);
-#endif
         const bool was_inf = inf;
         ec_accumulate<ILP>(acc, inf, acc.z, tx, ty, take);
         // only the first nonzero digit of a lane starts from infinity: skip
         // the 24 selects in every window where no lane of the wave does
         if (__any(take && was_inf)) gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
       }
-      // G terms every fifth window (radix 2^20): slot 0 = u1_lo * G,
-      // slot 1 = u1_hi * 2^128 G; entries were DMA'd into LDS before the doublings.
-      if (gwin) {
-#pragma unroll 1
-        for (int slot = 0; slot < 2; ++slot) {
-          if (SPLIT && slot != half) continue;
-          const uint32_t gd = slot == 0 ? gd0 : gd1;
-          const bool take = (gd & GD_MAG) != 0;
-          fe tx, ty;
-          {
-            const int gs = SPLIT ? 0 : slot;
-            const uint4 a0 = gpf[wv][gs][0][ln], a1 = gpf[wv][gs][1][ln];
-            const uint4 a2 = gpf[wv][gs][2][ln], a3 = gpf[wv][gs][3][ln];
-            tx.v[0] = a0.x; tx.v[1] = a0.y; tx.v[2] = a0.z; tx.v[3] = a0.w;
-            tx.v[4] = a1.x; tx.v[5] = a1.y; tx.v[6] = a1.z; tx.v[7] = a1.w;
-            ty.v[0] = a2.x; ty.v[1] = a2.y; ty.v[2] = a2.z; ty.v[3] = a2.w;
-            ty.v[4] = a3.x; ty.v[5] = a3.y; ty.v[6] = a3.z; ty.v[7] = a3.w;
-          }
-#if HKV_CNEG
-          fe_cneg(ty, ty, (gd & GD_NEG) != 0);
-#else
-          fe nty;
-          fe_neg(nty, ty);
-          fe_cmov(ty, nty, (gd & GD_NEG) != 0);
-#endif
-          fe az;
-          fe_mul(az, acc.z, Zg);
-          const bool was_inf = inf;
-          ec_accumulate<ILP>(acc, inf, az, tx, ty, take);
-          if (__any(take && was_inf)) {  // map the G-multiple onto the accumulator's curve
-            fe zg2;
-            fe_sqr(zg2, Zg);
-            fe_mul(tx, tx, zg2);
-            fe_mul(zg2, zg2, Zg);
-            fe_mul(ty, ty, zg2);
-            gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
-          }
-        }
-      }
       dw = dw_next;
     }
 
-    if (SPLIT) {
-      // half 1 hands (X, Y, Z, inf) to half 0 through LDS: word-major [25][128]
-      uint32_t* xch = reinterpret_cast<uint32_t*>(&gpf[0][0][0][0]);
-      __syncthreads();  // every wave is past its last read of gpf
-      if (half == 1) {
+    if (!SPLIT) {  // hand B' = (X, Y, Z acc * Zg) on E_w to the finish kernel
+      fe zt;
+      fe_mul(zt, acc.z, Zg);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          xch[k * PER_WG + sub] = acc.x.v[k];
-          xch[(8 + k) * PER_WG + sub] = acc.y.v[k];
-          xch[(16 + k) * PER_WG + sub] = acc.z.v[k];
-        }
-        xch[24 * PER_WG + sub] = inf ? 1u : 0u;
+      for (int k = 0; k < 8; ++k) {
+        im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
+        im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
+        im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
       }
-      __syncthreads();
-      if (half == 0) {
-        gej b;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          b.x.v[k] = xch[k * PER_WG + sub];
-          b.y.v[k] = xch[(8 + k) * PER_WG + sub];
-          b.z.v[k] = xch[(16 + k) * PER_WG + sub];
-        }
-        const bool binf = xch[24 * PER_WG + sub] != 0;
-        // acc + b, both Jacobian on the same isomorphic curve: rescale acc by
-        // b.z (same point), then b enters as (X2, Y2) against scale Z1
-        gej a2;
-        fe z2, z3;
-        fe_sqr(z2, b.z);
-        fe_mul(z3, z2, b.z);
-        fe_mul(a2.x, acc.x, z2);
-        fe_mul(a2.y, acc.y, z3);
-        fe_mul(a2.z, acc.z, b.z);
-        bool ainf = inf;
-        gej_accumulate(a2, ainf, acc.z, b.x, b.y, !binf && !inf);
-        // acc = inf: the sum is b; b = inf: the sum is acc
-        const bool take_b = inf && !binf;
-        const bool keep_a = binf;
-        gej_cmov(a2, b, take_b);
-        gej_cmov(a2, acc, keep_a);
-        acc = a2;
-        inf = keep_a ? inf : (take_b ? false : ainf);
-      }
-      __syncthreads();  // the next window loop's G DMA reuses gpf
-    }
-
-#if HKV_YFREE || HKV_SPLIT_YFREE
-    if (SPLIT ? HKV_SPLIT_YFREE == 1 : HKV_YFREE) {  // hand B' = (X, Y, Z acc * Zg) on E_w on
-      if (!SPLIT || half == 0) {                 // (finish kernel / split join kernel)
-        fe zt;
-        fe_mul(zt, acc.z, Zg);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
-          im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
-          im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
-        }
-        im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
-      }
-#if HKV_FUSE_FINISH && HKV_YFREE
-      if (!SPLIT) finish_lane(im, n, n_pad, gtab, rare_ctr, i, flags | (inf ? FLAG_BINF : 0u));
-#endif
+      im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
       continue;
     }
-#endif
-    // ---- inversion-free x compare ----
-    bool accept = false;
-#if HKV_SPLIT_YFREE == 2
-    if (SPLIT) {  // B = phi^-1(B') = (X, Y, Z acc Zg y0) on E, R = A + B exactly, x compare
-      if (half == 0) {
-        gej A, b;
-        fe y0;
-        uint32_t r[8];
+
+    // ---- SPLIT: the halves meet; B = phi^-1(B') = (X, Y, Z acc Zg y0) on E,
+    // R = A + B exactly, x compare ----
+    if (half == 1) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
-          A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
-          A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
-          y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
-          r[k] = im[(size_t)(IM_R + k) * n_pad + i];
-        }
-        const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
-        b.x = acc.x;
-        b.y = acc.y;
-        fe zt;
-        fe_mul(zt, acc.z, Zg);
-        fe_mul(b.z, zt, y0);
-        bool rinf = (af & AUXF_AINF) != 0;
-        gej_add_var(A, rinf, b, inf);
-        accept = valid && (af & AUXF_SQ) && !rinf && x_matches_r(A.x, A.z, r);
+      for (int k = 0; k < 8; ++k) {
+        xch[k * PER_WG + sub] = acc.x.v[k];
+        xch[(8 + k) * PER_WG + sub] = acc.y.v[k];
+        xch[(16 + k) * PER_WG + sub] = acc.z.v[k];
       }
-    } else
-#endif
-    {
-      sc r;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) r.v[k] = im[(size_t)(IM_R + k) * n_pad + i];
-      fe zt, zz, X, t, rf;
-      fe_mul(zt, acc.z, Zg);
-      fe_sqr(zz, zt);
-      X = acc.x;
-      fe_normalize(X);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) rf.v[k] = r.v[k];
-      fe_mul(t, rf, zz);
-      fe_normalize(t);
-      bool eq = fe_eq_norm(t, X);
-      // r + n < p ?
-      const bool small_r = u256_lt(r.v, PMN);
-      uint32_t c = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) rf.v[k] = addc(r.v[k], SC_N[k], c);
-      fe_mul(t, rf, zz);
-      fe_normalize(t);
-      eq = eq || (small_r && fe_eq_norm(t, X));
-      accept = valid && !inf && eq;
+      xch[24 * PER_WG + sub] = inf ? 1u : 0u;
     }
+    __syncthreads();  // barrier A
+    bool accept = false;
+    if (half == 0) {
+      gej b;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        b.x.v[k] = xch[k * PER_WG + sub];
+        b.y.v[k] = xch[(8 + k) * PER_WG + sub];
+        b.z.v[k] = xch[(16 + k) * PER_WG + sub];
+      }
+      const bool binf = xch[24 * PER_WG + sub] != 0;
+      // acc + b, both Jacobian on the same isomorphic curve: rescale acc by
+      // b.z (same point), then b enters as (X2, Y2) against scale Z1
+      gej_add_var(acc, inf, b, binf);
+      gej A;
+      fe y0;
+      uint32_t r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
+        A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
+        A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
+        y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+        r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+      }
+      const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
+      gej bb;
+      bb.x = acc.x;
+      bb.y = acc.y;
+      fe zt;
+      fe_mul(zt, acc.z, Zg);
+      fe_mul(bb.z, zt, y0);
+      bool rinf = (af & AUXF_AINF) != 0;
+      gej_add_var(A, rinf, bb, inf);
+      accept = valid && (af & AUXF_SQ) && !rinf && x_matches_r(A.x, A.z, r);
+    }
+    __syncthreads();  // barrier B: the next signature group's writers of xch / aux wait for the readers
     const uint64_t ball = __ballot(accept);
     if ((threadIdx.x & 63) == 0 && half == 0) {
       // n_words bounds the caller's bitmap ((n + 31) / 32 words when the
@@ -1035,7 +798,6 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
   }
 }
 
-#if HKV_YFREE
 // ---------------------------------------------------------------------------
 // 2b. y-free finish (full-grid batches). The ecmult kernel leaves
 //   B' = u2 * Q' = (X, Y, Z) on E_w : y^2 = x^3 + 7 w^3, Q' = (x w, w^2) =
@@ -1098,11 +860,8 @@ HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]) {
 #define HKV_VERDICT_BATCH 16
 #endif
 constexpr int VERDICT_BATCH = HKV_VERDICT_BATCH;
-// den^-1: Bernstein-Yang safegcd mod p (hkv_safegcd.h, 750 divsteps) instead of
-// the Fermat chain (255S + 15M)
-#ifndef HKV_VERDICT_SAFEGCD
-#define HKV_VERDICT_SAFEGCD 1
-#endif
+// den^-1: Bernstein-Yang safegcd mod p (hkv_safegcd.h); it replaced the
+// Fermat chain (255S + 15M): verdict kernel 160 -> 135 us at 1M
 #ifndef HKV_FINISH_WAVES
 #define HKV_FINISH_WAVES 3  // waves per SIMD the finish kernel's register allocation targets: 3 (168 VGPRs,
                             // 180 B/lane spilled) is 0.8% faster than 2 (208 VGPRs), 4 (179 VGPRs spilled)
@@ -1129,16 +888,7 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
   uint32_t gd = valid ? im[(size_t)IM_GDIG * n_pad + i] : 0u;
   fe tx, ty;
   gtab_entry(gtab, 0, gd, tx, ty);
-#if HKV_CNEG
   fe_cneg(A.y, ty, (gd & GD_NEG) != 0);
-#else
-  {
-    fe nty;
-    fe_neg(nty, ty);
-    A.y = ty;
-    fe_cmov(A.y, nty, (gd & GD_NEG) != 0);
-  }
-#endif
   A.x = tx;
   fe_set_u32(A.z, 1);
   ainf = (gd & GD_MAG) == 0;
@@ -1150,13 +900,7 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
     fe nx, nyy;
     if (t + 1 < 2 * GWIN) gtab_entry(gtab, t + 1, gdn, nx, nyy);
     const bool take = (gd & GD_MAG) != 0;
-#if HKV_CNEG
     fe_cneg(ty, ty, (gd & GD_NEG) != 0);
-#else
-    fe nty;
-    fe_neg(nty, ty);
-    fe_cmov(ty, nty, (gd & GD_NEG) != 0);
-#endif
     const bool was_inf = ainf;
     gej_accumulate(A, ainf, A.z, tx, ty, take);
     if (__any(take && was_inf)) gej_accumulate_from_inf(A, ainf, tx, ty, take && was_inf);
@@ -1166,9 +910,8 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
   }
 }
 
-// one signature's finish (hkv_finish_kernel, or the ecmult kernel's own
-// tail with HKV_FUSE_FINISH): whole waves call it (the rare-lane compaction
-// ballots)
+// one signature's finish (hkv_finish_kernel): whole waves call it (the
+// rare-lane compaction ballots)
 HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
                          uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags) {
   const bool valid = (i < n) && (flags & FLAG_VALID);
@@ -1363,12 +1106,8 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
     }
   }
   fe inv;
-#if HKV_VERDICT_SAFEGCD
   fe_normalize(c);  // safegcd wants 0 < c < p
   sgcd::inv_mod_p(inv.v, c.v);
-#else
-  fe_inv(inv, c);
-#endif
   struct Ops {
     uint32_t f;
     fe prev, d, num, w;
@@ -1425,77 +1164,6 @@ __global__ void __launch_bounds__(WG) hkv_yverdict_kernel(uint32_t* __restrict__
     }
   }
 }
-#if HKV_SPLIT_YFREE
-// Small batches, y-free (HKV_SPLIT_YFREE): beside the split ecmult (which
-// leaves B' = u2 Q' on E_w), hkv_gsqrt_kernel runs on an auxiliary stream:
-// A = u1 G from the per-window tables and the key's y0 = sqrt(w) with the
-// key's parity (no root: the key does not parse). hkv_split_join_kernel then
-// maps B' back to E as (X, Y, Z y0) (phi^-1), adds A exactly and compares.
-// The square root thus leaves the small-batch critical path.
-__global__ void __launch_bounds__(WG) hkv_gsqrt_kernel(const uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
-                                                       const uint32_t* __restrict__ gtab, uint32_t* __restrict__ aux) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n_pad) return;
-  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-  const bool valid = (i < n) && (flags & FLAG_VALID);
-  gej A;
-  bool ainf;
-  gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
-  fe w, y0, y2, ny;
-  im_load8(im, n_pad, IM_W, i, w.v);
-  fe_sqrt_cand(y0, w);
-  fe_sqr(y2, y0);
-  const bool is_sq = fe_equal(y2, w);
-  fe_normalize(y0);
-  fe_neg(ny, y0);
-  fe_normalize(ny);
-  if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
-    aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
-    aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
-    aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
-  }
-  aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
-}
-
-__global__ void __launch_bounds__(WG) hkv_split_join_kernel(const uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
-                                                            const uint32_t* __restrict__ aux,
-                                                            uint32_t* __restrict__ bits, uint32_t n_words) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;  // n_pad % WG == 0: whole waves
-  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-  const bool valid = (i < n) && (flags & FLAG_VALID);
-  gej A, B;
-  fe y0;
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    B.x.v[k] = im[(size_t)(IM_BX + k) * n_pad + i];
-    B.y.v[k] = im[(size_t)(IM_BX + 8 + k) * n_pad + i];
-    B.z.v[k] = im[(size_t)(IM_BX + 16 + k) * n_pad + i];
-    A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
-    A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
-    A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
-    y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
-    r[k] = im[(size_t)(IM_R + k) * n_pad + i];
-  }
-  const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
-  gej b = B;
-  fe_mul(b.z, B.z, y0);  // B = phi^-1(B') = (X, Y, Z y0) on E
-  bool rinf = (af & AUXF_AINF) != 0;
-  gej_add_var(A, rinf, b, (flags & FLAG_BINF) != 0);
-  const bool accept = valid && (af & AUXF_SQ) && !rinf && x_matches_r(A.x, A.z, r);
-  const uint64_t ball = __ballot(accept);
-  if ((threadIdx.x & 63) == 0) {
-    const uint32_t wi = i / 32;
-    if (wi < n_words) bits[wi] = (uint32_t)ball;
-    if (wi + 1 < n_words) bits[wi + 1] = (uint32_t)(ball >> 32);
-  }
-}
-#endif
-#endif
-
 // ---------------------------------------------------------------------------
 // shared helpers for table init / generators: simple MSB-first double-and-add
 // with complete additions (slow, used off the timed path only).
@@ -1851,45 +1519,39 @@ namespace hkv {
 
 static inline uint32_t ceil_div(size_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
-hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im, bool split,
+hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* im,
                            hipStream_t st) {
-  if (split) {  // n_pad % WG == 0: n_pad / 128 workgroups of 128 signatures
-    hipLaunchKernelGGL(hkv_prologue_split_kernel, dim3(n_pad / (WG / 2)), dim3(WG), 0, st, (const uint32_t*)recs, n,
-                       n_pad, mode, im);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(hkv_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st,
                      (const uint32_t*)recs, n, n_pad, mode, im);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // BATCH_INV signatures per lane at large n; small batches (a block) keep
-  // at least 65,536 lanes (or one per signature) so the latency of the
-  // sequential batch products does not dominate
+  // BATCH_INV signatures per lane at large n; smaller batches keep at least
+  // 65,536 lanes (or one per signature) so the latency of the sequential
+  // batch products does not dominate
   uint32_t stride = ceil_div(n_pad, BATCH_INV);
   stride = stride > 65536u ? stride : (n_pad < 65536u ? n_pad : 65536u);
   hipLaunchKernelGGL(hkv_inv_kernel, dim3(ceil_div(stride, WG)), dim3(WG), 0, st, n_pad, stride, im);
   e = hipGetLastError();
-  if (e != hipSuccess || HKV_INV_GLV) return e;
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
-#ifndef HKV_MID_ILP
-#define HKV_MID_ILP 1  // mid-size full-grid batches use the paired forms
-#endif
+// split: small batches (SPLIT_SIGS signatures per workgroup, no separate
+// prologue); mid: full-grid batches of at most 2 waves per SIMD, the
+// paired-form instance at a 2-wave register allocation
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
-                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool ilp,
-                         unsigned long long* clk, uint32_t* rare_ctr, uint32_t* aux, const void* recs,
-                         uint32_t mode, hipStream_t st) {
+                         uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool mid,
+                         unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st) {
   const uint32_t* rw = (const uint32_t*)recs;
   if (split)
-    hipLaunchKernelGGL((hkv_ecmult_kernel<true, HKV_SPLIT_ILP != 0>), dim3(grid), dim3(SPLIT_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, clk, rare_ctr, aux, rw, mode);
-  else if (ilp && HKV_MID_ILP)
+    hipLaunchKernelGGL((hkv_ecmult_kernel<true, true>), dim3(grid), dim3(SPLIT_TPB), 0, st, im, n, n_pad, gtab, qs,
+                       bits, n_words, clk, aux, rw, mode);
+  else if (mid)
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, rare_ctr, aux, rw, mode);
+                       n_words, clk, aux, rw, mode);
   else
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, rare_ctr, aux, rw, mode);
+                       n_words, clk, aux, rw, mode);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {
@@ -1902,35 +1564,11 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
                      gtab);
   return hipGetLastError();
 }
-hipError_t launch_gsqrt(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* aux,
-                        hipStream_t st) {
-#if HKV_SPLIT_YFREE
-  hipLaunchKernelGGL(hkv_gsqrt_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, aux);
-  return hipGetLastError();
-#else
-  (void)im; (void)n; (void)n_pad; (void)gtab; (void)aux; (void)st;
-  return hipSuccess;
-#endif
-}
-hipError_t launch_split_join(const uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* aux, uint32_t* bits,
-                             uint32_t n_words, hipStream_t st) {
-#if HKV_SPLIT_YFREE
-  hipLaunchKernelGGL(hkv_split_join_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, aux, bits, n_words);
-  return hipGetLastError();
-#else
-  (void)im; (void)n; (void)n_pad; (void)aux; (void)bits; (void)n_words; (void)st;
-  return hipSuccess;
-#endif
-}
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st) {
-#if HKV_YFREE
-  hipError_t e = hipSuccess;
-  if (!HKV_FUSE_FINISH) {
-    hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, rare_ctr);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
+  hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, rare_ctr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad, (const uint32_t*)rare_ctr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1944,10 +1582,6 @@ hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
   hipLaunchKernelGGL(hkv_yverdict_kernel, dim3(stride / WG), dim3(WG), 0, st, im, n_pad, stride, bits, n_words,
                      rare_ctr);
   return hipGetLastError();
-#else
-  (void)im; (void)n; (void)n_pad; (void)gtab; (void)rare_ctr; (void)bits; (void)n_words; (void)st;
-  return hipSuccess;
-#endif
 }
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st) {
   hipLaunchKernelGGL(hkv_gen_pool_kernel, dim3(ceil_div(npool, WG)), dim3(WG), 0, st, seed, npool, pool);

@@ -64,31 +64,18 @@ constexpr uint32_t DIG_ZERO = (uint32_t)QBIAS | ((uint32_t)QBIAS << QDIG_BITS);
 constexpr int BATCH_INV = HKV_BATCH_INV;
 constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF = 8u;
 
-// y-free verification (HKV_YFREE, full-grid batches; hkv_kernels.hip §2b):
-// the prologue stores w = x^3 + 7 over IM_QY instead of solving y = sqrt(w);
+// y-free verification (every launch shape; hkv_kernels.hip §2b): the
+// prologue stores w = x^3 + 7 over IM_QY instead of solving y = sqrt(w);
 // ecmult runs u2 * Q' on E_w : y^2 = x^3 + 7 w^3 with Q' = (x w, w^2) and
 // leaves B' = (X, Y, Z) over the Q-digit words; the finish kernel adds the
 // u1 * G sum from per-window tables and reduces "x(u1 G + u2 Q) == r" to
-// y_c = num / den, accepted iff y_c^2 == w with the key's y parity.
-#ifndef HKV_YFREE
-#define HKV_YFREE 1
-#endif
-// Small batches (the split ecmult) y-free too (HKV_SPLIT_YFREE): the key's
-// square root leaves the prologue's critical path and runs beside the split
-// ecmult (hkv_gsqrt_kernel on an auxiliary stream, with the u1 * G sum);
-// hkv_split_join_kernel maps B' back with y0 and compares. Mode 1 (that aux
-// stream) is correct but its kernel is not reliably concurrent with the split
-// ecmult (configs[2] block 798 -> 772 us, configs[0] block 754 -> 872 us);
-// mode 2 (default) runs the same work as waves 4-5 of the split kernel's own
-// workgroups: configs[0] 755 -> 703 us, configs[2] 796 -> 744 us
-// (profiles/r02_variants_split_yfree.log).
-#ifndef HKV_SPLIT_YFREE
-#define HKV_SPLIT_YFREE 2
-#endif
-static_assert(!HKV_SPLIT_YFREE || HKV_YFREE, "the split y-free path uses the y-free helpers and tables");
-// HKV_SPLIT_YFREE=2: the u1 * G sum and the square root run as waves 4-5 of
-// the split kernel's own workgroups (384 threads), so they are concurrent by
-// construction; the join and the compare stay in that kernel.
+// y_c = num / den, accepted iff y_c^2 == w with the key's y parity. Small
+// batches (the split ecmult) run the u1 * G sum and the key's square root as
+// waves 4-5 of each workgroup, beside the two Q chains, and join exactly in
+// the kernel (configs[0] block 755 -> 703 us, configs[2] 796 -> 744 us;
+// profiles/r02_variants_split_yfree.log); waves 4-5 also parse the
+// signatures while waves 0-3 build the Q tables (configs[0] 701 -> 696 us,
+// profiles/r02_variants_split_fuse.log).
 // HKV_SPLIT_SIGS: signatures per split workgroup (128: waves 0-1 / 2-3 / 4-5
 // are the halves and the G-sum waves; 64: one wave each, 192 threads)
 #ifndef HKV_SPLIT_SIGS
@@ -96,18 +83,8 @@ static_assert(!HKV_SPLIT_YFREE || HKV_YFREE, "the split y-free path uses the y-f
 #endif
 static_assert(HKV_SPLIT_SIGS == 64 || HKV_SPLIT_SIGS == 128, "split workgroups take 64 or 128 signatures");
 constexpr int SPLIT_SIGS = HKV_SPLIT_SIGS;
-constexpr int SPLIT_TPB = (HKV_SPLIT_YFREE == 2 ? 3 : 2) * SPLIT_SIGS;
-// HKV_SPLIT_FUSE: split batches skip hkv_prologue_split_kernel; waves 4-5 of
-// the split ecmult parse the signature (s^-1, u1, u2, GLV, digits) while
-// waves 0-3 parse the key and build their tables, one barrier apart.
-// configs[0] block 701 -> 696 us, configs[2] 743 -> 736 us: the signature
-// half (~65 us of one wave's issue) stays ahead of the chains, only the table
-// build overlaps (profiles/r02_variants_split_fuse.log).
-#ifndef HKV_SPLIT_FUSE
-#define HKV_SPLIT_FUSE 1
-#endif
-static_assert(!HKV_SPLIT_FUSE || HKV_SPLIT_YFREE == 2, "the fused split prologue runs in waves 4-5");
-// hkv_gsqrt_kernel's output (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
+constexpr int SPLIT_TPB = 3 * SPLIT_SIGS;
+// waves 4-5's output for the join (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
 enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_WORDS = 33 };
 constexpr uint32_t AUXF_AINF = 1u, AUXF_SQ = 2u;
 constexpr uint32_t FLAG_YODD = 16u;      // the key's y is odd (prefix 03/07, or the 04 key's y)
@@ -130,13 +107,11 @@ static_assert(IM_RARE_LIST < IM_R, "A and the rare list fit below r");
 static_assert(IM_DIG + 24 <= IM_GDIG, "B' and num/den fit over the Q digits");
 
 // Fixed-base tables in HBM: multiples j*B for j = 1..2^19, affine, 16 dwords
-// per entry [x(8) | y(8)], table t at entry offset t*2^19. Tables 0 and 1
-// (64 MiB, MALL resident) are B = G and 2^128 G: the split ecmult gathers
-// them per lane by LDS-DMA at the start of the window that adds them (four
-// doublings ahead). With HKV_YFREE, tables 2j + h (j = 1..GWIN-1) hold
-// B = 2^(GTAB_W j + 128 h) G, so the finish kernel sums u1 * G without doublings.
+// per entry [x(8) | y(8)], table t at entry offset t*2^19: table 2j + h holds
+// B = 2^(GTAB_W j + 128 h) G (j = 0..GWIN-1), so the u1 * G sum (finish
+// kernel, split waves 4-5) takes one addition per table and no doublings.
 constexpr int GTAB_ENTRIES = 1 << (GTAB_W - 1);
-constexpr int GTAB_TABLES = HKV_YFREE ? 2 * GWIN : 2;
+constexpr int GTAB_TABLES = 2 * GWIN;
 constexpr size_t GTAB_DWORDS = (size_t)GTAB_TABLES * GTAB_ENTRIES * 16;
 
 // Per-lane Q table: multiples j*Q, j = 1..QBIAS, affine on the lane's isomorphic

@@ -193,7 +193,7 @@ __constant__ static const uint32_t GLV_LAMBDA[8] = {0x1B23BD72u, 0xDF02967Cu, 0x
 // c = round(k * g / 2^384): bits 384..511 of the product plus bit 383.
 HKV_DEV void glv_round(sc& c, const sc& k, const uint32_t* g) {
   uint32_t t[16];
-  mul256(t, k.v, g);
+  mul512(t, k.v, g);
   uint32_t rnd = t[11] >> 31;
   uint32_t cy = rnd;
   c.v[0] = addc(t[12], 0u, cy);
