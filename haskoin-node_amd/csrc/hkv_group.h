@@ -194,6 +194,127 @@ HKV_DEV void gej_accumulate_ilp(gej& acc, bool& inf, const fe& az, const fe& tx,
   }
 }
 
+// ---- pair-lane forms: one point on two lanes (2c, 2c + 1) ----
+// A wave that runs alone on its SIMD is issue-bound on the field products
+// (fe_mul: 880 SIMD cycles at one wave, the interleaved pair fe_mul2 1,740:
+// profiles/r02_ubench_field_mulred.json), so two independent products of one
+// point operation cost the same whether they sit in one lane or not — unless
+// they sit in TWO lanes of the same instruction stream. The pair forms keep
+// a Jacobian point as P = X (even lane) | Y (odd lane) and Z on the odd lane,
+// and run each step's independent products on the two lanes at once; the
+// operands move between the lanes with DPP quad permutations (fe_xch: swap
+// within the pair, fe_bc1: the odd lane's value on both) and lane-parity
+// selects (fe_sel, a bitfield insert with the all-ones odd-lane mask).
+// A doubling is then 2S + 2M deep instead of 4S + 3M, a mixed addition
+// 1S + 5M instead of 3S + 8M. Both lanes of a pair always take the same
+// branches (their flags are made pair-uniform), so every DPP source lane is
+// active.
+HKV_DEV uint32_t dpp_xch(uint32_t v) {  // quad_perm [1, 0, 3, 2]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+HKV_DEV uint32_t dpp_bc1(uint32_t v) {  // quad_perm [1, 1, 3, 3]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false);
+}
+HKV_DEV uint32_t dpp_bc0(uint32_t v) {  // quad_perm [0, 0, 2, 2]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);
+}
+HKV_DEV void fe_xch(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = dpp_xch(a.v[i]);
+}
+HKV_DEV void fe_bc1(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = dpp_bc1(a.v[i]);
+}
+// r = a on the even lane, b on the odd lane (odd: all ones on odd lanes)
+HKV_DEV void fe_sel(fe& r, const fe& a, const fe& b, uint32_t odd) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = (a.v[i] & ~odd) | (b.v[i] & odd);
+}
+// a flag computed on one lane of the pair, made pair-uniform
+HKV_DEV bool pair_even(bool f) { return dpp_bc0(f ? 1u : 0u) != 0; }
+HKV_DEV bool pair_odd(bool f) { return dpp_bc1(f ? 1u : 0u) != 0; }
+
+// 2(X, Y, Z) in the halved form of gej_double (the same point scaled by 1/2)
+HKV_DEV void pair_double(fe& P, fe& Z, uint32_t odd) {
+  fe R1, T, O, R2, E, R3, U, X3, D, t;
+  fe_sqr(R1, P);              // A = X^2        | B = Y^2
+  fe_xch(T, R1);              // B              | A
+  fe_sel(O, T, Z, odd);       // B              | Z
+  fe_mul(R2, P, O);           // M = X B        | Z3' = Y Z
+  fe_mul_small(E, T, 3);
+  fe_half(E, E);              //                | E' = 3A/2
+  fe_sel(O, T, E, odd);       // B              | E'
+  fe_sqr(R3, O);              // C = B^2        | E'^2
+  fe_xch(U, R3);              // E'^2           | C
+  fe_shl(t, R2, 1);
+  fe_sub(X3, U, t);           // X3' = E'^2 - 2M
+  fe_sub(D, R2, X3);          // M - X3'
+  fe_xch(t, D);               //                | M - X3'
+  fe_mul(t, E, t);            //                | E'(M - X3')
+  fe_sub(t, t, U);            //                | Y3' = E'(M - X3') - C
+  fe_sel(P, X3, t, odd);
+  Z = R2;                     //                | Z3'
+}
+
+// The pair form of gej_accumulate: (P, Z, inf) += T with T = TXY = tx (even
+// lane) | ty (odd lane), affine on the curve of Jacobian scale Z (the
+// accumulator's own isomorphic curve). take must be pair-uniform; lanes at
+// infinity are left to pair_accumulate_from_inf.
+HKV_DEV void pair_accumulate(fe& P, fe& Z, bool& inf, const fe& TXY, bool take, uint32_t odd) {
+  fe z2, O1, O2, R2, H, R3, Rr;
+  fe_sqr(z2, Z);              //                | Z^2
+  fe_bc1(O2, z2);             // Z^2            | Z^2
+  fe_sel(O1, TXY, Z, odd);    // tx             | Z
+  fe_mul(R2, O1, O2);         // U2 = tx Z^2    | Z^3
+  fe_sub(H, R2, P);           // H = U2 - X1
+  fe_sel(O1, H, TXY, odd);    // H              | ty
+  fe_sel(O2, H, R2, odd);     // H              | Z^3
+  fe_mul(R3, O1, O2);         // H^2            | S2 = ty Z^3
+  fe_sub(Rr, R3, P);          //                | R = S2 - Y1
+  const bool live = take && !inf;
+  const bool hz = pair_even(fe_is_zero(H));
+  if (live && !hz) {
+    fe R5, R6, W, X3, D, R7, t;
+    fe_sel(O1, H, Rr, odd);   // H              | R
+    fe_sel(O2, R3, Rr, odd);  // H^2            | R
+    fe_mul(R5, O1, O2);       // H^3            | R^2
+    fe_xch(t, H);             //                | H
+    fe_sel(O1, P, Z, odd);    // X1             | Z1
+    fe_sel(O2, R3, t, odd);   // H^2            | H
+    fe_mul(R6, O1, O2);       // V = X1 H^2     | Z3 = Z1 H
+    fe_xch(W, R5);            // R^2            | H^3
+    fe_sub(X3, W, R5);
+    fe_shl(t, R6, 1);
+    fe_sub(X3, X3, t);        // X3 = R^2 - H^3 - 2V
+    fe_sub(D, R6, X3);        // V - X3
+    fe_xch(t, D);             //                | V - X3
+    fe_xch(O1, P);            // Y1             | X1
+    fe_sel(O1, O1, Rr, odd);  // Y1             | R
+    fe_sel(O2, R5, t, odd);   // H^3            | V - X3
+    fe_mul(R7, O1, O2);       // Y1 H^3         | R (V - X3)
+    fe_xch(t, R7);
+    fe_sub(t, R7, t);         //                | Y3 = R (V - X3) - Y1 H^3
+    fe_sel(P, X3, t, odd);
+    Z = R6;                   //                | Z3
+  }
+  const bool degen = live && hz;
+  if (__builtin_expect(__any(degen), 0)) {
+    const bool rz = pair_odd(fe_is_zero(Rr));
+    if (degen && rz) pair_double(P, Z, odd);   // T == acc
+    inf = inf || (degen && !rz);               // T == -acc
+  }
+}
+// (P, Z) := (TXY, 1) on pairs that take a point while at infinity
+HKV_DEV void pair_accumulate_from_inf(fe& P, fe& Z, bool& inf, const fe& TXY, bool take) {
+  const bool f = take && inf;
+  fe_cmov(P, TXY, f);
+  fe one;
+  fe_set_u32(one, 1);
+  fe_cmov(Z, one, f);
+  inf = inf && !take;
+}
+
 // acc := (itx, ity, 1) on lanes that take a point while at infinity
 HKV_DEV void gej_accumulate_from_inf(gej& acc, bool& inf, const fe& itx, const fe& ity, bool take) {
   const bool f = take && inf;

@@ -799,6 +799,294 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
 }
 
 // ---------------------------------------------------------------------------
+// 2c. Pair-lane split kernel (small batches: a block). A workgroup takes
+//     PAIR_SIGS = 32 signatures on 4 waves, one per SIMD of its CU:
+//       wave 0: k1 * Q' chains, two lanes per signature (pair form,
+//               hkv_group.h pair_double / pair_accumulate), then the join;
+//       wave 1: k2 * lambda(Q') chains, two lanes per signature;
+//       wave 2: signature parse (s^-1, u1, u2, GLV, digits; lanes 0-31),
+//               then A = u1 G from the per-window tables;
+//       wave 3: the key's y0 = sqrt(w) of its parity (lanes 0-31).
+//     Barrier P publishes the digits, A (wave 2) and y0 (wave 3) reach the
+//     join through aux, half 1's sum through LDS (barrier A); barrier B ends
+//     the group. Every chain wave runs alone on its SIMD, where it is
+//     issue-bound: the pair forms put each step's independent products on two
+//     lanes of one instruction stream.
+// ---------------------------------------------------------------------------
+constexpr int PAIR_SIGS = 32;
+constexpr int PAIR_TPB = 256;
+// compress the even bits of a 64-bit lane mask into 32 bits (signature c = lanes 2c, 2c + 1)
+HKV_DEV uint32_t even_bits(uint64_t x) {
+  x &= 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+  return (uint32_t)x;
+}
+__global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* __restrict__ im, uint32_t n,
+                                                                     uint32_t n_pad,
+                                                                     const uint32_t* __restrict__ gtab,
+                                                                     uint32_t* __restrict__ qs,
+                                                                     uint32_t* __restrict__ bits, uint32_t n_words,
+                                                                     uint32_t* __restrict__ aux,
+                                                                     const uint32_t* __restrict__ recs,
+                                                                     uint32_t mode) {
+  // per chain wave: QTAB_ENTRIES entries x 8 words x 64 lanes (each lane keeps
+  // its own coordinate of every entry: x or beta*x on the even lane, y on the odd)
+  __shared__ uint32_t qlds[2][QTAB_ENTRIES][8][64];
+  __shared__ uint32_t xch[25 * PAIR_SIGS];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ln = threadIdx.x & 63;
+  const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
+  const uint32_t n_lanes = gridDim.x * 128u;        // chain lanes of the launch (qs scratch)
+  const uint32_t qlane = blockIdx.x * 128u + (threadIdx.x & 127u);
+
+  for (uint32_t base = blockIdx.x * PAIR_SIGS; base < n_pad; base += gridDim.x * PAIR_SIGS) {
+    if (wv == 2) {
+      // ---- signature parse (lanes 0-31), then A = u1 G ----
+      const uint32_t i = base + ln;
+      uint32_t flags = 0;
+      if (ln < PAIR_SIGS) {
+        bool ok, glv_ok, n1, n2;
+        sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
+        uint32_t kw[REC_WORDS];
+#pragma unroll
+        for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+        fe x, w;
+        uint32_t pflags = 0;
+        const bool pk = pubkey_parse_rec_w(kw, x, w, pflags) && i < n;
+        flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
+        im[(size_t)IM_FLAGS * n_pad + i] = flags;
+        __threadfence_block();
+      }
+      __syncthreads();  // barrier P
+      if (ln < PAIR_SIGS) {
+        gej A;
+        bool ainf;
+        gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
+          aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
+          aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
+        }
+        aux[(size_t)AUX_FLAGS * n_pad + i] = ainf ? AUXF_AINF : 0u;
+        __threadfence_block();
+      }
+      __syncthreads();  // barrier A
+      __syncthreads();  // barrier B
+      continue;
+    }
+    if (wv == 3) {
+      // ---- the key's y0 = sqrt(w) with the key's y parity (lanes 0-31) ----
+      __syncthreads();  // barrier P (nothing to wait for: the key bytes are input)
+      const uint32_t i = base + ln;
+      if (ln < PAIR_SIGS) {
+        uint32_t kw[REC_WORDS];
+#pragma unroll
+        for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+        fe x, w, y0, y2, ny;
+        uint32_t pflags = 0;
+        (void)pubkey_parse_rec_w(kw, x, w, pflags);
+        fe_sqrt_cand(y0, w);
+        fe_sqr(y2, y0);
+        const bool is_sq = fe_equal(y2, w);
+        fe_normalize(y0);
+        fe_neg(ny, y0);
+        fe_normalize(ny);
+        if ((y0.v[0] & 1u) != ((pflags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
+        aux[(size_t)AUX_SQ * n_pad + i] = is_sq ? AUXF_SQ : 0u;
+        __threadfence_block();
+      }
+      __syncthreads();  // barrier A
+      __syncthreads();  // barrier B
+      continue;
+    }
+
+    // ---- chain waves: half = wv (0: k1 * Q', 1: k2 * lambda(Q')) ----
+    const int half = wv;
+    const uint32_t c = ln >> 1;                    // signature of the pair
+    const uint32_t i = base + c;
+    uint32_t kw[REC_WORDS];
+#pragma unroll
+    for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+    ge q;
+    {
+      fe w;
+      uint32_t pflags;
+      const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
+      fe xw, ww;  // Q' = (x w, w^2) on E_w
+      fe_mul(xw, q.x, w);
+      fe_sqr(ww, w);
+      q.x = xw;
+      q.y = ww;
+      if (!pk) ge_set_g(q);  // dummy point (the lane is invalid: its digits are zero)
+    }
+    // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale
+    // Zg (both lanes of the pair build it; each keeps its coordinate in LDS) ----
+    fe Zg;
+    {
+      gej p2, pj;
+      gej_set_ge(p2, q);
+      gej_double(p2, p2);  // 2Q (Jacobian, scale Z2)
+      fe z2, qx, qy;       // Q' = phi_Z2(Q) = (x Z2^2, y Z2^3)
+      fe_sqr(z2, p2.z);
+      fe_mul(qx, q.x, z2);
+      fe_mul(z2, z2, p2.z);
+      fe_mul(qy, q.y, z2);
+      qtab_store(qs, n_lanes, qlane, 0, 0, qx);
+      qtab_store(qs, n_lanes, qlane, 0, 2, qy);
+      qtab_store(qs, n_lanes, qlane, 1, 0, p2.x);
+      qtab_store(qs, n_lanes, qlane, 1, 2, p2.y);
+      pj.x = p2.x;
+      pj.y = p2.y;
+      fe_set_u32(pj.z, 1);
+#pragma unroll 1
+      for (int j = 2; j < QTAB_ENTRIES; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
+        bool hz, rz;
+        fe h;
+        gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
+        qtab_store(qs, n_lanes, qlane, j, 0, pj.x);
+        qtab_store(qs, n_lanes, qlane, j, 2, pj.y);
+        qtab_store(qs, n_lanes, qlane, (j - 1), 4, h);
+      }
+      fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
+      fe beta;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) beta.v[k] = FE_BETA[k];
+      auto put = [&](int j, const fe& x, const fe& y) {
+        fe v;
+        fe_sel(v, x, y, odd);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qlds[half][j][k][ln] = v.v[k];
+      };
+      {
+        fe bx = pj.x;
+        if (half) fe_mul(bx, pj.x, beta);
+        put(QTAB_ENTRIES - 1, bx, pj.y);
+      }
+      fe rho;
+      fe_set_u32(rho, 1);
+#pragma unroll 1
+      for (int j = QTAB_ENTRIES - 2; j >= 0; --j) {
+        fe x, y, t;
+        if (j >= 1) {
+          qtab_load(qs, n_lanes, qlane, j, 4, t);  // H_{j+1}
+          fe_mul(rho, rho, t);
+        }
+        qtab_load(qs, n_lanes, qlane, j, 0, x);
+        qtab_load(qs, n_lanes, qlane, j, 2, y);
+        fe_sqr(t, rho);
+        fe_mul(x, x, t);
+        fe_mul(t, t, rho);
+        fe_mul(y, y, t);
+        if (half) fe_mul(x, x, beta);
+        put(j, x, y);
+      }
+    }
+    __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
+    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+    const bool valid = (i < n) && (flags & FLAG_VALID);
+    const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
+
+    // ---- the chain: 33 radix-16 windows, pair form ----
+    fe P, Z;
+    bool inf = true;
+    fe_set_zero(P);
+    fe_set_zero(Z);
+    uint32_t dw = valid ? im[(size_t)(IM_DIG + NWIN - 1) * n_pad + i] : DIG_ZERO;
+#pragma unroll 1
+    for (int win = NWIN - 1; win >= 0; --win) {
+      const int dg = half ? (int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS : (int)(dw & QDIG_MASK) - QBIAS;
+      const int mg = dg < 0 ? -dg : dg;
+      const int ie = mg ? mg - 1 : 0;
+      const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
+      if (win != NWIN - 1) {
+#pragma unroll 1
+        for (int d = 0; d < QW; ++d) {
+          if (!inf) pair_double(P, Z, odd);
+        }
+      }
+      const bool take = dg != 0;
+      const bool neg = (dg < 0) != negh;
+      fe T;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) T.v[k] = qlds[half][ie][k][ln];
+      fe_cneg(T, T, neg && odd);  // y -> -y on the odd lane
+      const bool was_inf = inf;
+      pair_accumulate(P, Z, inf, T, take, odd);
+      if (__any(take && was_inf)) pair_accumulate_from_inf(P, Z, inf, T, take && was_inf);
+      dw = dw_next;
+    }
+
+    // ---- join: half 1's sum to half 0 through LDS ----
+    if (half == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (!odd) xch[k * PAIR_SIGS + c] = P.v[k];
+        else {
+          xch[(8 + k) * PAIR_SIGS + c] = P.v[k];
+          xch[(16 + k) * PAIR_SIGS + c] = Z.v[k];
+        }
+      }
+      if (odd) xch[24 * PAIR_SIGS + c] = inf ? 1u : 0u;
+    }
+    fe Y, Zx;
+    fe_xch(Y, P);   // even lane: Y of the pair
+    fe_xch(Zx, Z);  // even lane: Z of the pair
+    __syncthreads();  // barrier A: half 1's sum, A and y0 are published
+    bool accept = false;
+    if (half == 0) {  // both lanes compute; the even lane's result is the verdict
+      gej acc, b;
+      acc.x = P;
+      acc.y = Y;
+      acc.z = Zx;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        b.x.v[k] = xch[k * PAIR_SIGS + c];
+        b.y.v[k] = xch[(8 + k) * PAIR_SIGS + c];
+        b.z.v[k] = xch[(16 + k) * PAIR_SIGS + c];
+      }
+      const bool binf = xch[24 * PAIR_SIGS + c] != 0;
+      gej_add_var(acc, inf, b, binf);  // B' = u2 Q' on E_w (iso scale Zg)
+      gej A;
+      fe y0;
+      uint32_t r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
+        A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
+        A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
+        y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+        r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+      }
+      const bool ainf = aux[(size_t)AUX_FLAGS * n_pad + i] != 0;
+      const bool is_sq = aux[(size_t)AUX_SQ * n_pad + i] != 0;
+      // B = phi^-1(B') = (X, Y, Z Zg y0) on E, R = A + B exactly, x compare
+      gej bb;
+      bb.x = acc.x;
+      bb.y = acc.y;
+      fe zt;
+      fe_mul(zt, acc.z, Zg);
+      fe_mul(bb.z, zt, y0);
+      bool rinf = ainf;
+      gej_add_var(A, rinf, bb, inf);
+      accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r);
+    }
+    const uint64_t ball = __ballot(accept && !odd);
+    if (half == 0 && ln == 0) {
+      const uint32_t wi = base / 32;
+      if (wi < n_words) bits[wi] = even_bits(ball);
+    }
+    __syncthreads();  // barrier B: the next group's writers of xch / aux wait for the readers
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 2b. y-free finish (full-grid batches). The ecmult kernel leaves
 //   B' = u2 * Q' = (X, Y, Z) on E_w : y^2 = x^3 + 7 w^3, Q' = (x w, w^2) =
 //   phi(Q) for the isomorphism phi(x, y) = (y0^2 x, y0^3 y), y0 = the key's y,
@@ -1544,8 +1832,8 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st) {
   const uint32_t* rw = (const uint32_t*)recs;
   if (split)
-    hipLaunchKernelGGL((hkv_ecmult_kernel<true, true>), dim3(grid), dim3(SPLIT_TPB), 0, st, im, n, n_pad, gtab, qs,
-                       bits, n_words, clk, aux, rw, mode);
+    hipLaunchKernelGGL(hkv_pair_split_kernel, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad, gtab, qs,
+                       bits, n_words, aux, rw, mode);
   else if (mid)
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
                        n_words, clk, aux, rw, mode);

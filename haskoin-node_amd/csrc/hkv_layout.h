@@ -85,7 +85,7 @@ static_assert(HKV_SPLIT_SIGS == 64 || HKV_SPLIT_SIGS == 128, "split workgroups t
 constexpr int SPLIT_SIGS = HKV_SPLIT_SIGS;
 constexpr int SPLIT_TPB = 3 * SPLIT_SIGS;
 // waves 4-5's output for the join (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
-enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_WORDS = 33 };
+enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_SQ = 33, AUX_WORDS = 34 };  // AUX_SQ: the pair kernel's sqrt wave
 constexpr uint32_t AUXF_AINF = 1u, AUXF_SQ = 2u;
 constexpr uint32_t FLAG_YODD = 16u;      // the key's y is odd (prefix 03/07, or the 04 key's y)
 constexpr uint32_t FLAG_COMP = 32u;      // compressed key: x^3 + 7 not yet shown to be a square
