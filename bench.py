@@ -212,7 +212,26 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
         torch.cuda.synchronize()
         res[f"{name}_us"] = round(e0.elapsed_time(e1) * 1e3 / k, 1)
     res["inputs_per_s"] = round(db.n / (res["total_us"] * 1e-6), 1)
+    res["split_phases_us"] = split_phases(v, torch, run)
     return res, got
+
+
+PHASES = ("start", "k1_table", "barrier_P", "k1_chain", "barrier_A", "join", "sig_parse", "u1G", "key_sqrt",
+          "k2_table", "k2_chain")
+
+
+def split_phases(v, torch, run) -> dict:
+    """Phase boundaries of workgroup 0 of the small-batch (split) kernel in
+    one extra profiled call (hkv_profile_phases: constant-rate clock stamps,
+    microseconds after the kernel's start)."""
+    v.lib.hkv_profile_enable(v.ctx, 1)
+    run()
+    torch.cuda.synchronize()
+    stamps = (ctypes.c_uint64 * len(PHASES))()
+    tick = ctypes.c_double()
+    v.lib.hkv_profile_phases(v.ctx, 0, stamps, len(PHASES), ctypes.byref(tick))
+    v.lib.hkv_profile_enable(v.ctx, 0)
+    return {name: round((int(stamps[k]) - int(stamps[0])) * tick.value * 1e-3, 1) for k, name in enumerate(PHASES)}
 
 
 def block_mix(v, torch, steps: int) -> dict:

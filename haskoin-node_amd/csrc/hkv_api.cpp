@@ -21,6 +21,7 @@
 #include "../../include/hkv.h"
 #include "hkv_internal.h"
 #include "hkv_layout.h"
+#include "hkv_plan.h"
 
 namespace {
 
@@ -69,13 +70,14 @@ struct DevCtx {
   // optional per-kernel timing (hkv_profile_*): events on the launch stream
   bool profile = false;
   std::vector<hipEvent_t> ev;  // triples: before prologue, between, after ecmult
-  unsigned long long* clk = nullptr;  // ecmult clock probe (4 counters)
+  unsigned long long* clk = nullptr;  // ecmult clock probe (4 counters) + split-kernel phase stamps (12)
   int wall_khz = 0;                   // constant-rate counter frequency
   // The scratch above (im, bits, qs, txt, pool, staging) is shared by every
   // call on this device whatever stream it names: each call waits for the
   // previous user's work (this event) before enqueueing and records it after,
   // so calls on different streams run in enqueue order instead of racing.
   hipEvent_t last_use = nullptr;
+  uint32_t inject = 0;  // hkv_debug_fail_device: HKV_FAIL_* of this device's next host-batch shard
 };
 
 }  // namespace
@@ -90,6 +92,10 @@ struct hkv_ctx {
   // other entry points keep running on the device meanwhile.
   std::mutex mu;
   std::vector<std::unique_ptr<std::mutex>> tx_mu;
+  // host-batch failover (verify_from_host): devices still in use, and how
+  // many shards each has failed
+  std::vector<bool> healthy;
+  std::vector<uint32_t> failures;
 };
 struct hkv_batch {
   hkv_ctx* ctx = nullptr;
@@ -241,7 +247,8 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
-  HKV_TRY(hipMalloc(&d.clk, 4 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
+  HKV_TRY(hipMalloc(&d.clk, 16 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
+  HKV_TRY(hipMemsetAsync(d.clk, 0, 16 * sizeof(unsigned long long), d.stream), "hipMemset(clock probe)");
   HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 448 MiB at radix 2^20
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
@@ -510,6 +517,8 @@ int hkv_open_devices(const int* device_ids, int n_ids, uint32_t flags, hkv_ctx**
   hkv_ctx* ctx = new (std::nothrow) hkv_ctx();
   if (!ctx) return HKV_E_OOM;
   ctx->devs.resize(n_ids);
+  ctx->healthy.assign(n_ids, true);
+  ctx->failures.assign(n_ids, 0);
   for (int k = 0; k < n_ids; ++k) ctx->tx_mu.emplace_back(new (std::nothrow) std::mutex());
   for (auto& m : ctx->tx_mu)
     if (!m) {
@@ -547,6 +556,25 @@ void hkv_close(hkv_ctx* ctx) {
 
 int hkv_ctx_num_devices(const hkv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
 
+int hkv_device_healthy(hkv_ctx* ctx, int dev) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  return ctx->healthy[(size_t)dev] ? 1 : 0;
+}
+
+int hkv_device_failures(hkv_ctx* ctx, int dev) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  return (int)ctx->failures[(size_t)dev];
+}
+
+int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || when > HKV_FAIL_JOIN) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  ctx->devs[(size_t)dev].inject = when;
+  return HKV_OK;
+}
+
 int hkv_batch_alloc(hkv_ctx* ctx, size_t max_n, hkv_batch** out) {
   if (!ctx || !out || max_n == 0) return HKV_E_ARG;
   hkv_batch* b = new (std::nothrow) hkv_batch();
@@ -570,114 +598,121 @@ void hkv_batch_free(hkv_batch* b) {
 uint8_t* hkv_batch_records(hkv_batch* b) { return b ? b->host : nullptr; }
 size_t hkv_batch_capacity(const hkv_batch* b) { return b ? b->cap : 0; }
 
-// On an error part-way through a multi-device call, wait for every device
-// already touched (0..k) before returning: their async H2D copies still read
-// the caller's host records and their kernels still write d.hbits.
-static int fail_sync(hkv_ctx* ctx, size_t k, int rc) {
-  for (size_t j = 0; j <= k && j < ctx->devs.size(); ++j) {
-    DevCtx& d = ctx->devs[j];
-    (void)hipSetDevice(d.device);
-    (void)hipStreamSynchronize(d.copy_stream);
-    (void)hipStreamSynchronize(d.stream);
+// Stop using a device whose shard failed: wait (best effort) for its copy and
+// verify streams, whose async H2D copies still read the caller's host records
+// and whose kernels still write d.hbits.
+static void quiesce(DevCtx& d) {
+  (void)hipSetDevice(d.device);
+  (void)hipStreamSynchronize(d.copy_stream);
+  (void)hipStreamSynchronize(d.stream);
+}
+
+// One shard of a host batch on its device: H2D of the records pipelined with
+// the verify in chunks of whole resident grids (the copy stream moves chunk
+// c+1 over PCIe while the verify stream works on chunk c; an event orders each
+// verify after its own H2D), each chunk's verdict words to the pinned staging
+// right after its verify, before d.bits is reused. (One H2D then one verify
+// measured 15.84 ms against 13.09 ms pipelined for 1M records:
+// profiles/r01_bench_hostpath*.log.)
+static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& s, uint32_t mode,
+                              std::vector<hipEvent_t>& evs) {
+  if (d.inject == HKV_FAIL_ENQUEUE) {
+    d.inject = 0;
+    g_last_hip = "injected enqueue failure (hkv_debug_fail_device)";
+    return HKV_E_HIP;
   }
+  const size_t len = s.hi - s.lo;
+  hipError_t e0 = hipSetDevice(d.device);
+  int rc = e0 == hipSuccess ? scratch_acquire(d, d.stream) : hip_fail(e0, "hipSetDevice");
+  if (!rc) rc = scratch_acquire(d, d.copy_stream);
+  if (!rc && d.recs_cap < len) {
+    if (d.recs) (void)hipFree(d.recs);
+    d.recs = nullptr;
+    d.recs_cap = 0;
+    e0 = hipMalloc(&d.recs, len * hkv::REC_SIZE);
+    if (e0 != hipSuccess) rc = hip_fail(e0, "hipMalloc(records)");
+    else d.recs_cap = len;
+  }
+  const size_t words = (len + 31) / 32;
+  if (!rc && d.hbits_cap < words) {
+    if (d.hbits) (void)hipHostFree(d.hbits);
+    d.hbits = nullptr;
+    d.hbits_cap = 0;
+    e0 = hipHostMalloc(reinterpret_cast<void**>(&d.hbits), words * 4, hipHostMallocPortable);
+    if (e0 != hipSuccess) rc = hip_fail(e0, "hipHostMalloc(bits)");
+    else d.hbits_cap = words;
+  }
+  if (rc) return rc;
+  const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
+  const size_t chunk = len >= 2 * grid_lanes ? grid_lanes * std::max<size_t>(1, (len / 4) / grid_lanes) : len;
+  const uint8_t* src = host + s.lo * hkv::REC_SIZE;
+  for (size_t off = 0; off < len && !rc; off += chunk) {
+    const size_t cl = std::min(chunk, len - off);
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) evs.push_back(ev);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d.recs + off * hkv::REC_SIZE, src + off * hkv::REC_SIZE, cl * hkv::REC_SIZE,
+                         hipMemcpyHostToDevice, d.copy_stream);
+    if (e == hipSuccess) e = hipEventRecord(ev, d.copy_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(d.stream, ev, 0);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "H2D records");
+      break;
+    }
+    rc = enqueue_verify(d, d.recs + off * hkv::REC_SIZE, cl, mode, d.stream);
+    if (!rc) {
+      e = hipMemcpyAsync(d.hbits + off / 32, d.bits, (cl + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream);
+      if (e != hipSuccess) rc = hip_fail(e, "D2H bits");
+    }
+  }
+  // the copy stream must not run ahead into the next call's H2D while this
+  // call's verify still reads d.recs: it is ordered through last_use
+  if (!rc) rc = scratch_release(d, d.stream);
+  if (!rc) rc = scratch_acquire(d, d.copy_stream);
   return rc;
 }
 
+static int join_host_shard(DevCtx& d, const hkv::Shard& s, uint32_t* out, size_t out_words) {
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  HKV_TRY(hipStreamSynchronize(d.stream), "verify sync");
+  if (d.inject == HKV_FAIL_JOIN) {
+    d.inject = 0;
+    g_last_hip = "injected join failure (hkv_debug_fail_device)";
+    return HKV_E_HIP;
+  }
+  if (!hkv::merge_shard_words(out, out_words, d.hbits, s)) {
+    g_last_hip = "shard does not fit the verdict bitmap";
+    return HKV_E_INTERNAL;
+  }
+  return HKV_OK;
+}
+
+// Host batch over the context's healthy devices: contiguous 64-aligned
+// shards (hkv_plan.h), and on a device failure its shard is re-verified on
+// the devices still healthy (the failed device is left out of every later
+// call of the context: hkv_device_healthy). Blocking.
 static int verify_from_host(hkv_ctx* ctx, const uint8_t* host, size_t n, uint32_t mode, uint32_t* out) {
   if (!ctx || !host || !out || mode > HKV_MODE_HASKOIN) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   std::lock_guard<std::mutex> lock(ctx->mu);
-  const size_t nd = ctx->devs.size();
-  // contiguous shards, 64-aligned starts; the last shard takes the remainder
-  size_t per = round_up((n + nd - 1) / nd, 64);
-  struct Shard { size_t lo, hi; };
-  std::vector<Shard> shards;
-  for (size_t k = 0; k < nd; ++k) {
-    size_t lo = std::min(n, k * per), hi = std::min(n, lo + per);
-    shards.push_back({lo, hi});
-  }
-  std::vector<std::vector<hipEvent_t>> h2d_events(nd);
-  struct EventGuard {  // destroyed after the join below (or on an early error return)
+  std::vector<std::vector<hipEvent_t>> evs(ctx->devs.size());
+  struct EventGuard {  // destroyed after every join (or on an early return)
     std::vector<std::vector<hipEvent_t>>& e;
     ~EventGuard() {
       for (auto& v : e)
         for (auto ev : v) (void)hipEventDestroy(ev);
     }
-  } guard{h2d_events};
-  for (size_t k = 0; k < nd; ++k) {
-    DevCtx& d = ctx->devs[k];
-    const size_t len = shards[k].hi - shards[k].lo;
-    if (!len) continue;
-    hipError_t e0 = hipSetDevice(d.device);
-    int rc = e0 == hipSuccess ? scratch_acquire(d, d.stream) : hip_fail(e0, "hipSetDevice");
-    if (!rc) rc = scratch_acquire(d, d.copy_stream);
-    if (!rc && d.recs_cap < len) {
-      if (d.recs) (void)hipFree(d.recs);
-      d.recs = nullptr;
-      d.recs_cap = 0;
-      e0 = hipMalloc(&d.recs, len * hkv::REC_SIZE);
-      if (e0 != hipSuccess) rc = hip_fail(e0, "hipMalloc(records)");
-      else d.recs_cap = len;
-    }
-    const size_t words = (len + 31) / 32;
-    if (!rc && d.hbits_cap < words) {
-      if (d.hbits) (void)hipHostFree(d.hbits);
-      d.hbits = nullptr;
-      d.hbits_cap = 0;
-      e0 = hipHostMalloc(reinterpret_cast<void**>(&d.hbits), words * 4, hipHostMallocPortable);
-      if (e0 != hipSuccess) rc = hip_fail(e0, "hipHostMalloc(bits)");
-      else d.hbits_cap = words;
-    }
-    if (rc) return fail_sync(ctx, k, rc);
-    // Pipelined over chunks of whole resident grids: the copy stream moves
-    // chunk c+1 over PCIe while the verify stream works on chunk c (events
-    // order each verify after its own H2D); each chunk's verdict words go to
-    // the pinned staging right after its verify, before d.bits is reused.
-    // (one H2D then one verify measured 15.84 ms against 13.09 ms pipelined
-    // for 1M records: profiles/r01_bench_hostpath*.log)
-    const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
-    const size_t chunk = (len >= 2 * grid_lanes)
-                             ? grid_lanes * std::max<size_t>(1, (len / 4) / grid_lanes)
-                             : len;
-    const uint8_t* src = host + shards[k].lo * hkv::REC_SIZE;
-    std::vector<hipEvent_t>& evs = h2d_events[k];
-    for (size_t off = 0; off < len && !rc; off += chunk) {
-      const size_t cl = std::min(chunk, len - off);
-      hipEvent_t ev = nullptr;
-      hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-      if (e == hipSuccess) evs.push_back(ev);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(d.recs + off * hkv::REC_SIZE, src + off * hkv::REC_SIZE, cl * hkv::REC_SIZE,
-                           hipMemcpyHostToDevice, d.copy_stream);
-      if (e == hipSuccess) e = hipEventRecord(ev, d.copy_stream);
-      if (e == hipSuccess) e = hipStreamWaitEvent(d.stream, ev, 0);
-      if (e != hipSuccess) {
-        rc = hip_fail(e, "H2D records");
-        break;
-      }
-      rc = enqueue_verify(d, d.recs + off * hkv::REC_SIZE, cl, mode, d.stream);
-      if (!rc) {
-        e = hipMemcpyAsync(d.hbits + off / 32, d.bits, (cl + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream);
-        if (e != hipSuccess) rc = hip_fail(e, "D2H bits");
-      }
-    }
-    // the copy stream must not run ahead into the next call's H2D while this
-    // call's verify still reads d.recs: it is ordered through last_use
-    if (!rc) rc = scratch_release(d, d.stream);
-    if (!rc) rc = scratch_acquire(d, d.copy_stream);
-    if (rc) return fail_sync(ctx, k, rc);
-  }
-  for (size_t k = 0; k < nd; ++k) {
-    DevCtx& d = ctx->devs[k];
-    const size_t len = shards[k].hi - shards[k].lo;
-    if (!len) continue;
-    HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-    HKV_TRY(hipStreamSynchronize(d.stream), "verify sync");
-    const size_t words = (len + 31) / 32;
-    std::memcpy(out + shards[k].lo / 32, d.hbits, words * 4);
-  }
-  // clear bits past n in the last word (kernel already writes 0 for i >= n)
-  return HKV_OK;
+  } guard{evs};
+  const size_t out_words = (n + 31) / 32;
+  return hkv::run_with_failover(
+      n, ctx->healthy,
+      [&](const hkv::Shard& s) { return enqueue_host_shard(ctx->devs[(size_t)s.dev], host, s, mode, evs[(size_t)s.dev]); },
+      [&](const hkv::Shard& s) { return join_host_shard(ctx->devs[(size_t)s.dev], s, out, out_words); },
+      [&](int dev, int) {
+        quiesce(ctx->devs[(size_t)dev]);
+        ++ctx->failures[(size_t)dev];
+      });
 }
 
 int hkv_verify(hkv_ctx* ctx, hkv_batch* b, size_t n, uint32_t mode, uint32_t* verdict_bits) {
@@ -788,6 +823,17 @@ int hkv_profile_clock(hkv_ctx* ctx, int dev, double* sclk_mhz) {
   HKV_TRY(hipMemcpy(c, d.clk, sizeof(c), hipMemcpyDeviceToHost), "D2H clock probe");
   *sclk_mhz = 0;
   if (c[3] > c[1] && d.wall_khz > 0) *sclk_mhz = (double)(c[2] - c[0]) / ((double)(c[3] - c[1]) / (d.wall_khz * 1e-3));
+  return HKV_OK;
+}
+
+int hkv_profile_phases(hkv_ctx* ctx, int dev, uint64_t* stamps, size_t n, double* tick_ns) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !stamps || !tick_ns || n > 12) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  HKV_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (n) HKV_TRY(hipMemcpy(stamps, d.clk + 4, n * sizeof(uint64_t), hipMemcpyDeviceToHost), "D2H phase stamps");
+  *tick_ns = d.wall_khz > 0 ? 1e6 / d.wall_khz : 0.0;
   return HKV_OK;
 }
 

@@ -815,6 +815,9 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
 // ---------------------------------------------------------------------------
 constexpr int PAIR_SIGS = 32;
 constexpr int PAIR_TPB = 256;
+// phase-stamp slots (clk[4 + slot]; include/hkv.h hkv_profile_phases)
+enum : int { PH_START = 0, PH_TABLE0, PH_P, PH_CHAIN0, PH_A, PH_JOIN, PH_SIG, PH_GSUM, PH_SQRT, PH_TABLE1, PH_CHAIN1,
+             PH_COUNT };
 // compress the even bits of a 64-bit lane mask into 32 bits (signature c = lanes 2c, 2c + 1)
 HKV_DEV uint32_t even_bits(uint64_t x) {
   x &= 0x5555555555555555ull;
@@ -832,7 +835,8 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
                                                                      uint32_t* __restrict__ bits, uint32_t n_words,
                                                                      uint32_t* __restrict__ aux,
                                                                      const uint32_t* __restrict__ recs,
-                                                                     uint32_t mode) {
+                                                                     uint32_t mode,
+                                                                     unsigned long long* __restrict__ clk) {
   // per chain wave: QTAB_ENTRIES entries x 8 words x 64 lanes (each lane keeps
   // its own coordinate of every entry: x or beta*x on the even lane, y on the odd)
   __shared__ uint32_t qlds[2][QTAB_ENTRIES][8][64];
@@ -842,6 +846,13 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
   const uint32_t n_lanes = gridDim.x * 128u;        // chain lanes of the launch (qs scratch)
   const uint32_t qlane = blockIdx.x * 128u + (threadIdx.x & 127u);
+  // optional phase stamps of workgroup 0 (hkv_profile_phases): constant-rate
+  // clock at the phase boundaries of each wave, slot PH_*
+  const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
+  auto mark = [&](int slot) {
+    if (stamp) clk[4 + slot] = wall_clock64();
+  };
+  if (wv == 0) mark(PH_START);
 
   for (uint32_t base = blockIdx.x * PAIR_SIGS; base < n_pad; base += gridDim.x * PAIR_SIGS) {
     if (wv == 2) {
@@ -861,6 +872,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         im[(size_t)IM_FLAGS * n_pad + i] = flags;
         __threadfence_block();
       }
+      mark(PH_SIG);
       __syncthreads();  // barrier P
       if (ln < PAIR_SIGS) {
         gej A;
@@ -875,6 +887,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         aux[(size_t)AUX_FLAGS * n_pad + i] = ainf ? AUXF_AINF : 0u;
         __threadfence_block();
       }
+      mark(PH_GSUM);
       __syncthreads();  // barrier A
       __syncthreads();  // barrier B
       continue;
@@ -902,6 +915,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         aux[(size_t)AUX_SQ * n_pad + i] = is_sq ? AUXF_SQ : 0u;
         __threadfence_block();
       }
+      mark(PH_SQRT);
       __syncthreads();  // barrier A
       __syncthreads();  // barrier B
       continue;
@@ -988,7 +1002,9 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         put(j, x, y);
       }
     }
+    mark(half ? PH_TABLE1 : PH_TABLE0);
     __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
+    if (half == 0) mark(PH_P);
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
     const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
@@ -1023,6 +1039,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
       dw = dw_next;
     }
 
+    mark(half ? PH_CHAIN1 : PH_CHAIN0);
     // ---- join: half 1's sum to half 0 through LDS ----
     if (half == 1) {
 #pragma unroll
@@ -1039,6 +1056,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
     fe_xch(Y, P);   // even lane: Y of the pair
     fe_xch(Zx, Z);  // even lane: Z of the pair
     __syncthreads();  // barrier A: half 1's sum, A and y0 are published
+    if (half == 0) mark(PH_A);
     bool accept = false;
     if (half == 0) {  // both lanes compute; the even lane's result is the verdict
       gej acc, b;
@@ -1078,6 +1096,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
       accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r);
     }
     const uint64_t ball = __ballot(accept && !odd);
+    if (half == 0) mark(PH_JOIN);
     if (half == 0 && ln == 0) {
       const uint32_t wi = base / 32;
       if (wi < n_words) bits[wi] = even_bits(ball);
@@ -1833,7 +1852,7 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
   const uint32_t* rw = (const uint32_t*)recs;
   if (split)
     hipLaunchKernelGGL(hkv_pair_split_kernel, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad, gtab, qs,
-                       bits, n_words, aux, rw, mode);
+                       bits, n_words, aux, rw, mode, clk);
   else if (mid)
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
                        n_words, clk, aux, rw, mode);

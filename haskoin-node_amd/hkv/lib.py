@@ -65,6 +65,9 @@ EXPORTS = {
     "hkv_open_devices": (c_int, [POINTER(c_int), c_int, c_uint32, POINTER(c_void_p)]),
     "hkv_close": (None, [c_void_p]),
     "hkv_ctx_num_devices": (c_int, [c_void_p]),
+    "hkv_device_healthy": (c_int, [c_void_p, c_int]),
+    "hkv_device_failures": (c_int, [c_void_p, c_int]),
+    "hkv_debug_fail_device": (c_int, [c_void_p, c_int, c_uint32]),
     "hkv_batch_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "hkv_batch_free": (None, [c_void_p]),
     "hkv_batch_records": (POINTER(c_uint8), [c_void_p]),
@@ -76,7 +79,7 @@ EXPORTS = {
                                        c_void_p]),
     "hkv_gen_batch_device": (c_int, [c_void_p, c_int, c_uint64, c_uint64, c_size_t, c_uint32, c_uint32, c_uint32,
                                      c_void_p, c_void_p, c_void_p]),
-    "hkv_sighash":(c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p, c_void_p]),
+    "hkv_sighash": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p, c_void_p]),
     "hkv_sighash_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32, c_void_p,
                                    c_size_t, c_void_p, c_void_p]),
     "hkv_std_inputs_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
@@ -99,6 +102,7 @@ EXPORTS = {
     "hkv_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                  POINTER(c_uint64)]),
     "hkv_profile_clock": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double)]),
+    "hkv_profile_phases": (c_int, [c_void_p, c_int, POINTER(c_uint64), c_size_t, POINTER(ctypes.c_double)]),
     "hkv_strerror": (c_char_p, [c_int]),
     "hkv_last_hip_error": (c_char_p, []),
     "hkv_device_count": (c_int, []),

@@ -97,6 +97,19 @@ int hkv_open(int n_gpus, uint32_t flags, hkv_ctx** out);
 int hkv_open_devices(const int* device_ids, int n_ids, uint32_t flags, hkv_ctx** out);
 void hkv_close(hkv_ctx* ctx);
 int hkv_ctx_num_devices(const hkv_ctx* ctx);
+/* Device k of the context still takes host-batch shards (1) or has failed
+ * one (0); negative on a bad argument. */
+int hkv_device_healthy(hkv_ctx* ctx, int dev);
+/* Host-batch shards device k has failed (0 or 1: a failed device gets no
+ * more shards); negative on a bad argument. */
+int hkv_device_failures(hkv_ctx* ctx, int dev);
+/* Test hook: device k's next host-batch shard fails — HKV_FAIL_ENQUEUE
+ * before anything is enqueued, HKV_FAIL_JOIN after its work completed — as a
+ * HIP error would, exercising the failover of hkv_verify / hkv_verify_host. */
+#define HKV_FAIL_NONE 0u
+#define HKV_FAIL_ENQUEUE 1u
+#define HKV_FAIL_JOIN 2u
+int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when);
 
 /* Pinned host record buffer with room for max_n records. */
 int hkv_batch_alloc(hkv_ctx* ctx, size_t max_n, hkv_batch** out);
@@ -105,7 +118,12 @@ uint8_t* hkv_batch_records(hkv_batch* b);
 size_t hkv_batch_capacity(const hkv_batch* b);
 
 /* Verify records [0, n) of the batch. Shards contiguous 64-aligned index
- * ranges across the context's devices; writes ceil(n/32) words. Blocking. */
+ * ranges across the context's healthy devices; writes ceil(n/32) words.
+ * Blocking. Failover: when a device's shard fails (a HIP error while
+ * enqueueing or while waiting for it), that device is marked unhealthy for
+ * the rest of the context's life and its shard is re-verified on the devices
+ * still healthy; the call fails only when none is left (the last error, or
+ * HKV_E_NODEV once every device of the context is unhealthy). */
 int hkv_verify(hkv_ctx* ctx, hkv_batch* b, size_t n, uint32_t mode, uint32_t* verdict_bits);
 
 /* Same, from any host memory (copied through the context's staging). */
@@ -311,6 +329,14 @@ int hkv_profile_read(hkv_ctx* ctx, int dev, double* prologue_ms, double* ecmult_
  * clock64() / wall_clock64() deltas around its work (so the roofline can be
  * priced at the measured clock). Synchronises the device. */
 int hkv_profile_clock(hkv_ctx* ctx, int dev, double* sclk_mhz);
+
+/* Phase stamps of workgroup 0 of the last profiled small-batch (split)
+ * launch: n <= 12 constant-rate clock values (tick_ns nanoseconds per tick)
+ * at its phase boundaries — 0 start, 1 k1 table built, 2 past barrier P,
+ * 3 k1 chain done, 4 past barrier A, 5 join done, 6 signature parse done,
+ * 7 u1 G done, 8 key sqrt done, 9 k2 table built, 10 k2 chain done.
+ * Synchronises the device. */
+int hkv_profile_phases(hkv_ctx* ctx, int dev, uint64_t* stamps, size_t n, double* tick_ns);
 
 const char* hkv_strerror(int err);
 const char* hkv_last_hip_error(void);

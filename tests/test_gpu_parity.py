@@ -479,3 +479,40 @@ def test_scratch_ordered_across_streams(torch, ver):
     exp = np.ones(n, dtype=bool)
     exp[::3] = False
     assert (gb == exp).all()
+
+
+def test_multi_device_failover_reshards(torch, ver):
+    """SURVEY §5 failover of the host-batch path (hkv_plan.h
+    run_with_failover through hkv_verify_host): three device contexts on one
+    GPU; device 1's shard fails before it is enqueued and device 2's after
+    its work ran (hkv_debug_fail_device). Both are marked unhealthy, their
+    shards are re-verified on device 0, and the bitmap equals the
+    single-device one; the next call uses device 0 only; when device 0 fails
+    too the call returns HKV_E_HIP, and every later call HKV_E_NODEV."""
+    import hkv
+    from hkv.lib import HkvError
+    n = 3 * (1 << 18) + 4321
+    d = gen_device(torch, ver, n, seed=0x46414C4C)
+    host = d.cpu().numpy().copy()
+    rng = np.random.default_rng(13)
+    bad = rng.choice(n, size=n // 40, replace=False)
+    host[bad * 168 + 70] ^= 0x10                       # a bit of s: rejects
+    single = ver.verify_records(host, 1)
+    with hkv.Verifier(hkv.VerifierConfig(device_ids=[0, 0, 0], flags=1)) as v3:
+        lib = v3.lib
+        assert lib.hkv_debug_fail_device(v3.ctx, 1, 1) == 0   # HKV_FAIL_ENQUEUE
+        assert lib.hkv_debug_fail_device(v3.ctx, 2, 2) == 0   # HKV_FAIL_JOIN
+        got = v3.verify_records(host, 1)
+        assert (got == single).all(), np.nonzero(got != single)[0][:10]
+        assert [lib.hkv_device_healthy(v3.ctx, k) for k in range(3)] == [1, 0, 0]
+        assert [lib.hkv_device_failures(v3.ctx, k) for k in range(3)] == [0, 1, 1]
+        got = v3.verify_records(host, 0)
+        assert (got == ver.verify_records(host, 0)).all()
+        assert lib.hkv_debug_fail_device(v3.ctx, 0, 1) == 0
+        with pytest.raises(HkvError) as e:
+            v3.verify_records(host[: 1000 * 168], 1)
+        assert e.value.rc == -4                            # HKV_E_HIP: no device left
+        with pytest.raises(HkvError) as e:
+            v3.verify_records(host[: 1000 * 168], 1)
+        assert e.value.rc == -2                            # HKV_E_NODEV
+    assert not single[bad].any() and single.sum() == n - bad.size
