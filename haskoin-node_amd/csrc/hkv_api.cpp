@@ -156,6 +156,25 @@ int scratch_release(DevCtx& d, hipStream_t st) {
   return HKV_OK;
 }
 
+// the split kernels' A = u1 G, y0 and flags for the join (hkv_layout.h AUX_*)
+int ensure_aux(DevCtx& d, size_t n_pad, hipStream_t st) {
+  if (d.aux_n >= n_pad) return HKV_OK;
+  if (d.aux) {
+    HKV_TRY(hipStreamSynchronize(st), "aux sync");
+    (void)hipFree(d.aux);
+    d.aux = nullptr;
+    d.aux_n = 0;
+  }
+  HKV_TRY(hipMalloc(&d.aux, n_pad * hkv::AUX_WORDS * sizeof(uint32_t)), "hipMalloc(aux)");
+  d.aux_n = n_pad;
+  return HKV_OK;
+}
+
+// whether a batch of n runs the small-batch (split) kernels
+bool split_batch(const DevCtx& d, size_t n) {
+  return round_up(n, hkv::WG) <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
+}
+
 // enqueue the verify of n records at d_records; verdict words in out_bits
 // ((n + 31) / 32 words, device memory) or, when null, in d.bits
 int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st,
@@ -175,17 +194,11 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // Above that the duplicated doublings cost more than the chain saves
   // (measured: a 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms
   // unsplit; the bound itself re-measured in profiles/r02_split_threshold.log).
-  const bool split = n_pad <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
+  const bool split = split_batch(d, n);
   if (!split) HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
-  if (split && d.aux_n < n_pad) {  // waves 4-5's A = u1 G and y0 for the join (hkv_layout.h AUX_*)
-    if (d.aux) {
-      HKV_TRY(hipStreamSynchronize(st), "aux sync");
-      (void)hipFree(d.aux);
-      d.aux = nullptr;
-      d.aux_n = 0;
-    }
-    HKV_TRY(hipMalloc(&d.aux, n_pad * hkv::AUX_WORDS * sizeof(uint32_t)), "hipMalloc(aux)");
-    d.aux_n = n_pad;
+  if (split) {
+    rc = ensure_aux(d, n_pad, st);
+    if (rc) return rc;
   }
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
   // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
@@ -404,10 +417,41 @@ int wait_ms_total(DevCtx& d, hipStream_t st, uint64_t seq, uint64_t* total) {
 // host waits for the sum, after publishing this call's scratch use, and
 // re-taken before the multisig work is enqueued (the caller also holds the
 // device's tx lock, which guards txt and the multisig scratch across the gap).
+// Small batches of standard inputs in one verify launch (hkv_pair_split_kernel
+// <true>): the chains start from the parsed keys and signatures while the
+// signature wave computes the sighashes and script checks beside them.
+int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                             void* recs, uint32_t* out_bits, hipStream_t st) {
+  const size_t n_pad = round_up(n, hkv::WG);
+  int rc = ensure_dev_buffers(d, n_pad);
+  if (!rc) rc = ensure_aux(d, n_pad, st);
+  if (rc) return rc;
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  if (d.profile) {
+    for (auto& x : e) HKV_TRY(hipEventCreate(&x), "hipEventCreate");
+    HKV_TRY(hipEventRecord(e[0], st), "hipEventRecord");
+    HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
+  }
+  HKV_TRY(hkv::launch_std_verify_split(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
+                                       (uint32_t)n_pad, forkid, static_cast<uint8_t*>(recs), d.im, d.gtab, d.qs,
+                                       d.aux, out_bits, (uint32_t)((n + 31) / 32), d.profile ? d.clk : nullptr, st),
+          "std-input verify launch");
+  if (d.profile) {
+    HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
+    d.ev.insert(d.ev.end(), e, e + 3);
+  }
+  return HKV_OK;
+}
+
 int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
                               void* recs, uint32_t* out_bits, hipStream_t st,
                               std::unique_lock<std::mutex>* lk = nullptr) {
-  int rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  // small batches: tx index, then one fused launch (the multisig scan after
+  // it, off the block's critical path); larger ones: the extraction kernel,
+  // then the record verify
+  const bool fused = split_batch(d, n);
+  int rc = fused ? enqueue_tx_index(d, dt, st) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, st);
   if (rc) return rc;
   rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
   if (!rc) rc = grow(&d.ms[2], &d.ms_cap[2], n * 8, "hipMalloc(multisig offsets)");
@@ -425,8 +469,10 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
                               desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq, st),
           "multisig scan launch");
-  rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
-  if (rc) return rc;
+  if (!fused) {
+    rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
+    if (rc) return rc;
+  }
   uint64_t total = 0;
   if (lk) {
     rc = scratch_release(d, st);

@@ -33,6 +33,7 @@
 #include "hkv_hash.h"
 #include "hkv_layout.h"
 #include "hkv_internal.h"
+#include "hkv_sighash_dev.h"
 
 namespace hkv {
 
@@ -236,8 +237,7 @@ HKV_DEV void shr_bits(uint32_t* a, int b) {
 // Radix-2^QW / radix-2^20 Booth recoding (LSB first, MSB-first consumption in
 // the ecmult kernel): d = ((v + 1) >> 1) - ((v >> W) << W), v = bits
 // [pos-1, pos+W-1]; sum_w d_w 2^(QW w) reproduces the scalar (< 2^129).
-HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2,
-                          uint32_t* SL, uint32_t* SH) {
+HKV_DEV void write_qdigits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2) {
   constexpr uint32_t QM = (1u << QW) - 1u;
   uint32_t p1 = 0, p2 = 0;
 #pragma unroll 1
@@ -251,6 +251,8 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
     const int d2 = (int)((v2 + 1u) >> 1) - (int)((v2 >> QW) << QW);
     im[(size_t)(IM_DIG + w) * n_pad + i] = (uint32_t)(d1 + QBIAS) | ((uint32_t)(d2 + QBIAS) << QDIG_BITS);
   }
+}
+HKV_DEV void write_gdigits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* SL, uint32_t* SH) {
   uint32_t pl = 0, ph = 0;
 #pragma unroll 1
   for (int j = 0; j < GWIN; ++j) {
@@ -265,6 +267,11 @@ HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i,
     im[(size_t)(IM_GDIG + 2 * j) * n_pad + i] = (uint32_t)(dl < 0 ? -dl : dl) | (dl < 0 ? GD_NEG : 0u);
     im[(size_t)(IM_GDIG + 2 * j + 1) * n_pad + i] = (uint32_t)(dh < 0 ? -dh : dh) | (dh < 0 ? GD_NEG : 0u);
   }
+}
+HKV_DEV void write_digits(uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, uint32_t* S1, uint32_t* S2,
+                          uint32_t* SL, uint32_t* SH) {
+  write_qdigits(im, n_pad, i, S1, S2);
+  write_gdigits(im, n_pad, i, SL, SH);
 }
 
 // (at one wave per SIMD the loop is load-latency bound: each iteration's
@@ -374,16 +381,13 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 // the mode's high-S policy,
 // s^-1, u1 = m/s, u2 = r/s, the GLV split and the Booth digits; stores the
 // digits and r for lane i.
-HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_pad, uint32_t mode,
-                      uint32_t* __restrict__ im, uint32_t i, bool& ok, bool& glv_ok, bool& n1, bool& n2) {
-  uint32_t w[24];
-#pragma unroll
-  for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
-  sc r, s, m;
-  rec_be256(r.v, w, 32);
-  rec_be256(s.v, w, 64);
-  rec_be256(m.v, w, 0);
-  ok = (i < n) && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
+// The u2 half of a signature: compact-range checks, the mode's high-S policy,
+// s^-1, u2 = r/s, the GLV split of u2, the Q digits, r -> im. ok is the
+// caller's validity so far (updated); sinv is s^-1 (of 1 when !ok) for the u1
+// half (sig_lane_g).
+HKV_DEV void sig_lane_q(sc r, sc s, uint32_t mode, uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, bool& ok,
+                        bool& glv_ok, bool& n1, bool& n2, sc& sinv) {
+  ok = ok && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
   const bool high = sc_is_high(s);
   if (mode == HKV_MODE_HASKOIN) {
     sc ns;
@@ -393,23 +397,43 @@ HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_
     ok = ok && !high;  // secp256k1_ecdsa_verify rejects high-S
   }
   ok = ok && !u256_is_zero(r.v) && !u256_is_zero(s.v);
-  sc_cond_sub_n(m.v);  // m = msg32 mod n
   if (!ok) sc_set_u32(s, 1);
-  sc sinv, u1, u2;
+  sc u2;
   sc_inv(sinv, s);
-  sc_mul(u1, m, sinv);
   sc_mul(u2, r, sinv);
   uint32_t k1[5], k2[5];
   glv_ok = glv_split(u2, k1, n1, k2, n2);
   const bool use = ok && glv_ok;
-  uint32_t S1[5], S2[5], SL[4], SH[4];
+  uint32_t S1[5], S2[5];
 #pragma unroll
   for (int q = 0; q < 5; ++q) { S1[q] = use ? k1[q] : 0u; S2[q] = use ? k2[q] : 0u; }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
-  write_digits(im, n_pad, i, S1, S2, SL, SH);
+  write_qdigits(im, n_pad, i, S1, S2);
 #pragma unroll
   for (int k = 0; k < 8; ++k) im[(size_t)(IM_R + k) * n_pad + i] = r.v[k];
+}
+// The u1 half: m = msg32 mod n, u1 = m / s, the G digits (zero unless use).
+HKV_DEV void sig_lane_g(sc m, const sc& sinv, bool use, uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i) {
+  sc_cond_sub_n(m.v);  // m = msg32 mod n
+  sc u1;
+  sc_mul(u1, m, sinv);
+  uint32_t SL[4], SH[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
+  write_gdigits(im, n_pad, i, SL, SH);
+}
+// Both halves from a verify record (waves 4-5 of a split workgroup).
+HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_pad, uint32_t mode,
+                      uint32_t* __restrict__ im, uint32_t i, bool& ok, bool& glv_ok, bool& n1, bool& n2) {
+  uint32_t w[24];
+#pragma unroll
+  for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
+  sc r, s, m, sinv;
+  rec_be256(r.v, w, 32);
+  rec_be256(s.v, w, 64);
+  rec_be256(m.v, w, 0);
+  ok = i < n;
+  sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
+  sig_lane_g(m, sinv, ok && glv_ok, im, n_pad, i);
 }
 // flags as the full-grid kernels leave them (hkv_glv_kernel)
 HKV_DEV uint32_t split_flags(bool ok, uint32_t pk_ok, bool glv_ok, bool n1, bool n2) {
@@ -804,20 +828,29 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
 //       wave 0: k1 * Q' chains, two lanes per signature (pair form,
 //               hkv_group.h pair_double / pair_accumulate), then the join;
 //       wave 1: k2 * lambda(Q') chains, two lanes per signature;
-//       wave 2: signature parse (s^-1, u1, u2, GLV, digits; lanes 0-31),
-//               then A = u1 G from the per-window tables;
+//       wave 2: the u2 half of the signature (s^-1, u2, GLV, Q digits;
+//               lanes 0-31), then the u1 half and A = u1 G from the
+//               per-window tables;
 //       wave 3: the key's y0 = sqrt(w) of its parity (lanes 0-31).
-//     Barrier P publishes the digits, A (wave 2) and y0 (wave 3) reach the
+//     Barrier P publishes the Q digits, A (wave 2) and y0 (wave 3) reach the
 //     join through aux, half 1's sum through LDS (barrier A); barrier B ends
 //     the group. Every chain wave runs alone on its SIMD, where it is
 //     issue-bound: the pair forms put each step's independent products on two
 //     lanes of one instruction stream.
+//     STD (hkv_verify_std_inputs*): the signatures are standard inputs, not
+//     records. Every wave runs the cheap half of verifyStdInput for its
+//     inputs (std_parse: template, strict DER, the key bytes), so the chains
+//     start without waiting for any hash; wave 2 runs the other half (the
+//     HASH160 / SHA-256 script checks and the sighash, std_hash) after
+//     barrier P, beside the chains — u1 = m / s is the only thing that needs
+//     the message — and writes the input's verify record.
 // ---------------------------------------------------------------------------
 constexpr int PAIR_SIGS = 32;
 constexpr int PAIR_TPB = 256;
 // phase-stamp slots (clk[4 + slot]; include/hkv.h hkv_profile_phases)
-enum : int { PH_START = 0, PH_TABLE0, PH_P, PH_CHAIN0, PH_A, PH_JOIN, PH_SIG, PH_GSUM, PH_SQRT, PH_TABLE1, PH_CHAIN1,
-             PH_COUNT };
+enum : int { STAMP_START = 0, STAMP_TABLE0, STAMP_P, STAMP_CHAIN0, STAMP_A, STAMP_JOIN, STAMP_SIG, STAMP_GSUM,
+             STAMP_SQRT, STAMP_TABLE1, STAMP_CHAIN1, STAMP_COUNT };
+constexpr uint32_t AUXF_STDOK = 4u;  // STD: the script checks passed (aux AUX_FLAGS)
 // compress the even bits of a 64-bit lane mask into 32 bits (signature c = lanes 2c, 2c + 1)
 HKV_DEV uint32_t even_bits(uint64_t x) {
   x &= 0x5555555555555555ull;
@@ -828,53 +861,130 @@ HKV_DEV uint32_t even_bits(uint64_t x) {
   x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
   return (uint32_t)x;
 }
-__global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* __restrict__ im, uint32_t n,
+// the record words 24..41 (pklen, SEC1 bytes) of a parsed standard input's
+// key, as hkv_std_input_kernel writes them (zero when the parse failed)
+HKV_DEV void std_key_words(uint32_t kw[REC_WORDS], const StdIn& x) {
+#pragma unroll
+  for (int k = 0; k < 24; ++k) kw[k] = 0;
+#pragma unroll
+  for (int w = 0; w < 18; ++w) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int q = 4 * w + b;  // byte 96 + q of the record
+      uint32_t byte = 0;
+      if (q == 0) byte = x.pub_len;
+      else if ((uint32_t)(q - 1) < x.pub_len && q - 1 < 65) byte = x.pub[q - 1];
+      v |= byte << (8 * b);
+    }
+    kw[24 + w] = x.ok ? v : 0u;
+  }
+}
+// the standard-input operands (hkv_verify_std_inputs*)
+struct StdArgs {
+  const uint8_t* txs;
+  uint32_t n_tx;
+  const uint32_t* txt;
+  const uint8_t* scripts;
+  uint32_t scripts_len;
+  const hkv_input_job* jobs;
+  int32_t forkid;
+};
+
+template <bool STD>
+__global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                                      uint32_t n_pad,
                                                                      const uint32_t* __restrict__ gtab,
                                                                      uint32_t* __restrict__ qs,
                                                                      uint32_t* __restrict__ bits, uint32_t n_words,
                                                                      uint32_t* __restrict__ aux,
-                                                                     const uint32_t* __restrict__ recs,
+                                                                     uint32_t* __restrict__ recs,
                                                                      uint32_t mode,
-                                                                     unsigned long long* __restrict__ clk) {
+                                                                     unsigned long long* __restrict__ clk,
+                                                                     StdArgs sa) {
   // per chain wave: QTAB_ENTRIES entries x 8 words x 64 lanes (each lane keeps
   // its own coordinate of every entry: x or beta*x on the even lane, y on the odd)
   __shared__ uint32_t qlds[2][QTAB_ENTRIES][8][64];
   __shared__ uint32_t xch[25 * PAIR_SIGS];
+  __shared__ uint32_t shabuf[STD ? 16 * WG : 1];  // std_hash's per-lane SHA-256 blocks ([word][thread])
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
   const uint32_t n_lanes = gridDim.x * 128u;        // chain lanes of the launch (qs scratch)
   const uint32_t qlane = blockIdx.x * 128u + (threadIdx.x & 127u);
   // optional phase stamps of workgroup 0 (hkv_profile_phases): constant-rate
-  // clock at the phase boundaries of each wave, slot PH_*
+  // clock at the phase boundaries of each wave, slot STAMP_*
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
     if (stamp) clk[4 + slot] = wall_clock64();
   };
-  if (wv == 0) mark(PH_START);
+  if (wv == 0) mark(STAMP_START);
+  // the key words of signature i (record words 24..41; STD: parsed from its
+  // input, which x receives)
+  auto key_words = [&](uint32_t i, uint32_t kw[REC_WORDS], StdIn& x) {
+    if constexpr (STD) {
+      std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid);
+      std_key_words(kw, x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+    }
+  };
 
   for (uint32_t base = blockIdx.x * PAIR_SIGS; base < n_pad; base += gridDim.x * PAIR_SIGS) {
     if (wv == 2) {
-      // ---- signature parse (lanes 0-31), then A = u1 G ----
+      // ---- the signature: u2 half (lanes 0-31), then the u1 half and A = u1 G ----
       const uint32_t i = base + ln;
       uint32_t flags = 0;
+      bool use = false;
+      sc sinv, m;
+      StdIn x = {};
       if (ln < PAIR_SIGS) {
-        bool ok, glv_ok, n1, n2;
-        sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
+        bool ok = i < n, glv_ok, n1, n2;
         uint32_t kw[REC_WORDS];
+        key_words(i, kw, x);
+        sc r, s;
+        if constexpr (STD) {
 #pragma unroll
-        for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
-        fe x, w;
+          for (int k = 0; k < 8; ++k) { r.v[k] = x.r[k]; s.v[k] = x.s[k]; }
+          ok = ok && x.ok;
+        } else {
+          uint32_t w[24];
+#pragma unroll
+          for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
+          rec_be256(r.v, w, 32);
+          rec_be256(s.v, w, 64);
+          rec_be256(m.v, w, 0);
+        }
+        sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
+        use = ok && glv_ok;
+        fe kx, kwv;
         uint32_t pflags = 0;
-        const bool pk = pubkey_parse_rec_w(kw, x, w, pflags) && i < n;
+        const bool pk = pubkey_parse_rec_w(kw, kx, kwv, pflags) && i < n;
         flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
         im[(size_t)IM_FLAGS * n_pad + i] = flags;
         __threadfence_block();
       }
-      mark(PH_SIG);
+      mark(STAMP_SIG);
       __syncthreads();  // barrier P
+      uint32_t stdok = 0;
+      if constexpr (STD) {
+        // the script checks and the sighash (whole wave: block-synchronous SHA-256)
+        uint32_t* r32 = recs + (size_t)(ln < PAIR_SIGS && i < n ? i : 0) * REC_WORDS;
+        if (ln >= PAIR_SIGS) x.ok = false;
+        uint32_t d[8];
+        const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d);  // (writes r32 only when x.ok)
+        if (ln < PAIR_SIGS) {
+          if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
+          uint32_t w[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) w[k] = !x.ok ? 0u : (live ? d[k] : (k == 0 ? 1u : 0u));
+          rec_be256(m.v, w, 0);
+          stdok = x.ok ? AUXF_STDOK : 0u;
+        }
+      }
       if (ln < PAIR_SIGS) {
+        sig_lane_g(m, sinv, use, im, n_pad, i);
         gej A;
         bool ainf;
         gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
@@ -884,10 +994,10 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
           aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
           aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
         }
-        aux[(size_t)AUX_FLAGS * n_pad + i] = ainf ? AUXF_AINF : 0u;
+        aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | stdok;
         __threadfence_block();
       }
-      mark(PH_GSUM);
+      mark(STAMP_GSUM);
       __syncthreads();  // barrier A
       __syncthreads();  // barrier B
       continue;
@@ -898,8 +1008,8 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
       const uint32_t i = base + ln;
       if (ln < PAIR_SIGS) {
         uint32_t kw[REC_WORDS];
-#pragma unroll
-        for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+        StdIn xs = {};
+        key_words(i, kw, xs);
         fe x, w, y0, y2, ny;
         uint32_t pflags = 0;
         (void)pubkey_parse_rec_w(kw, x, w, pflags);
@@ -915,7 +1025,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         aux[(size_t)AUX_SQ * n_pad + i] = is_sq ? AUXF_SQ : 0u;
         __threadfence_block();
       }
-      mark(PH_SQRT);
+      mark(STAMP_SQRT);
       __syncthreads();  // barrier A
       __syncthreads();  // barrier B
       continue;
@@ -926,8 +1036,10 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
     const uint32_t c = ln >> 1;                    // signature of the pair
     const uint32_t i = base + c;
     uint32_t kw[REC_WORDS];
-#pragma unroll
-    for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+    {
+      StdIn xs = {};
+      key_words(i, kw, xs);
+    }
     ge q;
     {
       fe w;
@@ -1002,9 +1114,9 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         put(j, x, y);
       }
     }
-    mark(half ? PH_TABLE1 : PH_TABLE0);
+    mark(half ? STAMP_TABLE1 : STAMP_TABLE0);
     __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
-    if (half == 0) mark(PH_P);
+    if (half == 0) mark(STAMP_P);
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
     const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
@@ -1039,7 +1151,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
       dw = dw_next;
     }
 
-    mark(half ? PH_CHAIN1 : PH_CHAIN0);
+    mark(half ? STAMP_CHAIN1 : STAMP_CHAIN0);
     // ---- join: half 1's sum to half 0 through LDS ----
     if (half == 1) {
 #pragma unroll
@@ -1056,7 +1168,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
     fe_xch(Y, P);   // even lane: Y of the pair
     fe_xch(Zx, Z);  // even lane: Z of the pair
     __syncthreads();  // barrier A: half 1's sum, A and y0 are published
-    if (half == 0) mark(PH_A);
+    if (half == 0) mark(STAMP_A);
     bool accept = false;
     if (half == 0) {  // both lanes compute; the even lane's result is the verdict
       gej acc, b;
@@ -1082,7 +1194,8 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
         y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
         r[k] = im[(size_t)(IM_R + k) * n_pad + i];
       }
-      const bool ainf = aux[(size_t)AUX_FLAGS * n_pad + i] != 0;
+      const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
+      const bool ainf = (af & AUXF_AINF) != 0;
       const bool is_sq = aux[(size_t)AUX_SQ * n_pad + i] != 0;
       // B = phi^-1(B') = (X, Y, Z Zg y0) on E, R = A + B exactly, x compare
       gej bb;
@@ -1093,10 +1206,10 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_pair_split_kernel(uint32_t* _
       fe_mul(bb.z, zt, y0);
       bool rinf = ainf;
       gej_add_var(A, rinf, bb, inf);
-      accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r);
+      accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r) && (!STD || (af & AUXF_STDOK));
     }
     const uint64_t ball = __ballot(accept && !odd);
-    if (half == 0) mark(PH_JOIN);
+    if (half == 0) mark(STAMP_JOIN);
     if (half == 0 && ln == 0) {
       const uint32_t wi = base / 32;
       if (wi < n_words) bits[wi] = even_bits(ball);
@@ -1851,14 +1964,27 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st) {
   const uint32_t* rw = (const uint32_t*)recs;
   if (split)
-    hipLaunchKernelGGL(hkv_pair_split_kernel, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad, gtab, qs,
-                       bits, n_words, aux, rw, mode, clk);
+    hipLaunchKernelGGL(hkv_pair_split_kernel<false>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
+                       gtab, qs, bits, n_words, aux, const_cast<uint32_t*>(rw), mode, clk, StdArgs{});
   else if (mid)
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
                        n_words, clk, aux, rw, mode);
   else
     hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
                        n_words, clk, aux, rw, mode);
+  return hipGetLastError();
+}
+// small batches of standard inputs: parse, the Q chains, the script checks,
+// the sighash and the verdict in one launch (hkv_pair_split_kernel<true>);
+// txt must hold the batch's tx index rows and BIP143 hashes
+hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                                   uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
+                                   int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
+                                   uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
+                                   hipStream_t st) {
+  const StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid};
+  hipLaunchKernelGGL(hkv_pair_split_kernel<true>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad, gtab,
+                     qs, bits, n_words, aux, reinterpret_cast<uint32_t*>(recs), (uint32_t)HKV_MODE_HASKOIN, clk, sa);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {

@@ -35,533 +35,9 @@
 #include "hkv_internal.h"
 #include "../../include/hkv.h"
 
+#include "hkv_sighash_dev.h"
+
 namespace hkv {
-
-// ---------------------------------------------------------------------------
-// byte-level readers
-// ---------------------------------------------------------------------------
-// bounds-checked varint (the tx index parse); values >= 2^32 fail (no such
-// count or length fits a batch)
-HKV_DEV bool rd_varint(const uint8_t* p, uint32_t& off, uint32_t end, uint32_t& v) {
-  if (off >= end) return false;
-  const uint32_t t = p[off];
-  if (t < 0xFDu) {
-    v = t;
-    off += 1;
-    return true;
-  }
-  const uint32_t w = t == 0xFDu ? 2u : (t == 0xFEu ? 4u : 8u);
-  if (end - off < 1u + w) return false;
-  uint32_t lo = 0, hi = 0;
-  for (uint32_t k = 0; k < w; ++k) {
-    const uint32_t b = p[off + 1 + k];
-    if (k < 4) lo |= b << (8 * k);
-    else hi |= b;
-  }
-  if (hi) return false;
-  v = lo;
-  off += 1 + w;
-  return true;
-}
-// unchecked varint on a structure the index kernel already validated
-HKV_DEV uint32_t get_varint(const uint8_t* p, uint32_t& off) {
-  const uint32_t t = p[off];
-  if (t < 0xFDu) {
-    off += 1;
-    return t;
-  }
-  if (t == 0xFDu) {
-    const uint32_t v = p[off + 1] | (p[off + 2] << 8);
-    off += 3;
-    return v;
-  }
-  const uint32_t v = p[off + 1] | (p[off + 2] << 8) | (p[off + 3] << 16) | ((uint32_t)p[off + 4] << 24);
-  off += t == 0xFEu ? 5u : 9u;
-  return v;
-}
-HKV_DEV uint64_t varint_lit(uint32_t v, uint32_t& n) {
-  if (v < 0xFDu) {
-    n = 1;
-    return v;
-  }
-  if (v <= 0xFFFFu) {
-    n = 3;
-    return 0xFDull | ((uint64_t)v << 8);
-  }
-  n = 5;
-  return 0xFEull | ((uint64_t)v << 8);
-}
-
-// Script op scan (haskoin scriptOps): true if every push fits; counts
-// single-byte OP_CODESEPARATOR (0xab) ops outside push data.
-HKV_DEV bool script_scan(const uint8_t* s, uint32_t len, uint32_t& n_sep) {
-  uint32_t off = 0;
-  n_sep = 0;
-  while (off < len) {
-    const uint32_t op = s[off];
-    uint64_t ol = 1;
-    if (op >= 1u && op <= 75u) {
-      ol = 1 + op;
-    } else if (op == 0x4Cu) {
-      if (len - off < 2) return false;
-      ol = 2 + (uint64_t)s[off + 1];
-    } else if (op == 0x4Du) {
-      if (len - off < 3) return false;
-      ol = 3 + (uint64_t)(s[off + 1] | (s[off + 2] << 8));
-    } else if (op == 0x4Eu) {
-      if (len - off < 5) return false;
-      ol = 5 + (uint64_t)(s[off + 1] | (s[off + 2] << 8) | (s[off + 3] << 16) | ((uint32_t)s[off + 4] << 24));
-    } else if (op == 0xABu) {
-      ++n_sep;
-    }
-    if (ol > (uint64_t)(len - off)) return false;
-    off += (uint32_t)ol;
-  }
-  return true;
-}
-HKV_DEV uint32_t script_op_len(const uint8_t* s, uint32_t off) {
-  const uint32_t op = s[off];
-  if (op >= 1u && op <= 75u) return 1 + op;
-  if (op == 0x4Cu) return 2 + s[off + 1];
-  if (op == 0x4Du) return 3 + (s[off + 1] | (s[off + 2] << 8));
-  if (op == 0x4Eu) return 5 + (s[off + 1] | (s[off + 2] << 8) | (s[off + 3] << 16) | ((uint32_t)s[off + 4] << 24));
-  return 1;
-}
-
-// ---------------------------------------------------------------------------
-// preimage generator
-// ---------------------------------------------------------------------------
-enum : uint32_t {
-  PH_DONE = 0,
-  // txSigHash (legacy) preimage
-  PH_L_VER, PH_L_NIN, PH_L_IN_OP, PH_L_IN_SLEN, PH_L_IN_CODE, PH_L_IN_SEQ, PH_L_OUTS, PH_L_BLANK_A,
-  PH_L_BLANK_B, PH_L_LOCK, PH_L_SH,
-  // output walker (value, canonical script length, script), returns to g.ret
-  PH_O_VAL, PH_O_LEN, PH_O_SCRIPT,
-  // txSigHashForkId (BIP143) preimage
-  PH_F_VER, PH_F_HASH, PH_F_OUTPOINT, PH_F_SLEN, PH_F_CODE, PH_F_VALUE, PH_F_SEQ, PH_F_HO, PH_F_LOCK, PH_F_SH,
-  // per-tx BIP143 parts
-  PH_P_IN, PH_S_IN,
-  // a single byte range
-  PH_RANGE,
-};
-constexpr uint32_t GF_ACP = 1u, GF_ALL = 2u, GF_NONE = 4u, GF_SINGLE = 8u, GF_STRIP = 16u, GF_P2WPKH = 32u;
-
-struct Gen {
-  const uint8_t* src;  // current piece: byte range (src != null) or literal
-  uint64_t lit;
-  uint32_t rem;
-  uint32_t phase, ret;
-  const uint8_t* T;    // tx buffer (absolute offsets below)
-  uint32_t start, nin, nout, ins, outs_first, lock;
-  uint32_t i, shn, flags;
-  uint32_t j, ioff, seq_at, cnt;
-  uint32_t ooff, ocnt, osl, oscr;
-  uint32_t in_i, in_i_seq, single_off;
-  const uint8_t* code;
-  uint32_t code_len, code_out, ccur;
-  uint64_t value;
-  const uint32_t* hp;  // 32-byte hashes in digest byte order (null = zeros)
-  const uint32_t* hs;
-  const uint32_t* ho;
-};
-
-HKV_DEV void gen_clear(Gen& g) {
-  g.src = nullptr; g.lit = 0; g.rem = 0; g.phase = PH_DONE; g.ret = PH_DONE; g.T = nullptr;
-  g.start = g.nin = g.nout = g.ins = g.outs_first = g.lock = 0;
-  g.i = g.shn = g.flags = 0; g.j = g.ioff = g.seq_at = g.cnt = 0;
-  g.ooff = g.ocnt = g.osl = g.oscr = 0; g.in_i = g.in_i_seq = g.single_off = 0;
-  g.code = nullptr; g.code_len = g.code_out = g.ccur = 0; g.value = 0;
-  g.hp = g.hs = g.ho = nullptr;
-}
-HKV_DEV void piece_copy(Gen& g, const uint8_t* p, uint32_t n) { g.src = p; g.rem = n; }
-HKV_DEV void piece_lit(Gen& g, uint64_t v, uint32_t n) { g.src = nullptr; g.lit = v; g.rem = n; }
-HKV_DEV void piece_varint(Gen& g, uint32_t v) {
-  uint32_t n;
-  const uint64_t l = varint_lit(v, n);
-  piece_lit(g, l, n);
-}
-HKV_DEV void piece_hash(Gen& g, const uint32_t* h, uint32_t q) {
-  piece_lit(g, h ? ((uint64_t)h[2 * q] | ((uint64_t)h[2 * q + 1] << 32)) : 0ull, 8);
-}
-
-// Set up the next non-empty piece, or reach PH_DONE.
-HKV_DEV void gen_advance(Gen& g) {
-  const uint8_t* T = g.T;
-  switch (g.phase) {
-    // ---- txSigHash: serialize (tx copy) ++ LE32 sighash ----
-    case PH_L_VER: piece_copy(g, T + g.start, 4); g.phase = PH_L_NIN; break;
-    case PH_L_NIN:
-      piece_varint(g, (g.flags & GF_ACP) ? 1u : g.nin);
-      g.j = (g.flags & GF_ACP) ? g.i : 0u;
-      g.ioff = (g.flags & GF_ACP) ? g.in_i : g.ins;
-      g.phase = PH_L_IN_OP;
-      break;
-    case PH_L_IN_OP: {
-      piece_copy(g, T + g.ioff, 36);
-      uint32_t o = g.ioff + 36;
-      const uint32_t sl = get_varint(T, o);
-      g.seq_at = o + sl;
-      g.phase = PH_L_IN_SLEN;
-      break;
-    }
-    case PH_L_IN_SLEN:
-      if (g.j == g.i) {
-        piece_varint(g, g.code_out);
-        g.ccur = 0;
-        g.phase = PH_L_IN_CODE;
-      } else {
-        piece_lit(g, 0, 1);
-        g.phase = PH_L_IN_SEQ;
-      }
-      break;
-    case PH_L_IN_CODE:
-      if (!(g.flags & GF_STRIP)) {
-        piece_copy(g, g.code, g.code_len);
-        g.phase = PH_L_IN_SEQ;
-        break;
-      }
-      while (g.ccur < g.code_len) {  // drop OP_CODESEPARATOR ops
-        const uint32_t op = g.code[g.ccur];
-        const uint32_t ol = script_op_len(g.code, g.ccur);
-        if (op == 0xABu) {
-          g.ccur += 1;
-          continue;
-        }
-        piece_copy(g, g.code + g.ccur, ol);
-        g.ccur += ol;
-        return;
-      }
-      g.phase = PH_L_IN_SEQ;
-      break;
-    case PH_L_IN_SEQ:
-      if ((g.flags & GF_ALL) || g.j == g.i) piece_copy(g, T + g.seq_at, 4);
-      else piece_lit(g, 0, 4);
-      if (g.flags & GF_ACP) {
-        g.phase = PH_L_OUTS;
-      } else {
-        g.j += 1;
-        g.ioff = g.seq_at + 4;
-        g.phase = g.j < g.nin ? PH_L_IN_OP : PH_L_OUTS;
-      }
-      break;
-    case PH_L_OUTS:
-      if (g.flags & GF_ALL) {
-        piece_varint(g, g.nout);
-        g.ooff = g.outs_first;
-        g.ocnt = g.nout;
-        g.ret = PH_L_LOCK;
-        g.phase = PH_O_VAL;
-      } else if (g.flags & GF_NONE) {
-        piece_lit(g, 0, 1);
-        g.phase = PH_L_LOCK;
-      } else {
-        piece_varint(g, g.i + 1);
-        g.cnt = 0;
-        g.phase = PH_L_BLANK_A;
-      }
-      break;
-    case PH_L_BLANK_A:  // SINGLE: i outputs (2^64-1, empty script), then output i
-      if (g.cnt < g.i) {
-        piece_lit(g, ~0ull, 8);
-        g.phase = PH_L_BLANK_B;
-      } else {
-        g.ooff = g.single_off;
-        g.ocnt = 1;
-        g.ret = PH_L_LOCK;
-        g.phase = PH_O_VAL;
-      }
-      break;
-    case PH_L_BLANK_B: piece_lit(g, 0, 1); g.cnt += 1; g.phase = PH_L_BLANK_A; break;
-    case PH_L_LOCK: piece_copy(g, T + g.lock, 4); g.phase = PH_L_SH; break;
-    case PH_L_SH: piece_lit(g, g.shn, 4); g.phase = PH_DONE; break;
-    // ---- outputs ----
-    case PH_O_VAL: {
-      if (g.ocnt == 0) {
-        g.phase = g.ret;
-        break;
-      }
-      piece_copy(g, T + g.ooff, 8);
-      uint32_t o = g.ooff + 8;
-      g.osl = get_varint(T, o);
-      g.oscr = o;
-      g.phase = PH_O_LEN;
-      break;
-    }
-    case PH_O_LEN: piece_varint(g, g.osl); g.phase = PH_O_SCRIPT; break;
-    case PH_O_SCRIPT:
-      piece_copy(g, T + g.oscr, g.osl);
-      g.ooff = g.oscr + g.osl;
-      g.ocnt -= 1;
-      g.phase = PH_O_VAL;
-      break;
-    // ---- txSigHashForkId ----
-    case PH_F_VER: piece_copy(g, T + g.start, 4); g.cnt = 0; g.phase = PH_F_HASH; break;
-    case PH_F_HASH:
-      piece_hash(g, g.cnt < 4 ? g.hp : g.hs, g.cnt & 3u);
-      g.cnt += 1;
-      if (g.cnt == 8) g.phase = PH_F_OUTPOINT;
-      break;
-    case PH_F_OUTPOINT: piece_copy(g, T + g.in_i, 36); g.phase = PH_F_SLEN; break;
-    case PH_F_SLEN: piece_varint(g, g.code_len); g.cnt = 0; g.phase = PH_F_CODE; break;
-    case PH_F_CODE:
-      if (!(g.flags & GF_P2WPKH)) {
-        piece_copy(g, g.code, g.code_len);
-        g.phase = PH_F_VALUE;
-      } else if (g.cnt == 0) {  // scriptCode 76 a9 14 <h20> 88 ac of a P2WPKH program
-        piece_lit(g, 0x14A976ull, 3);
-        g.cnt = 1;
-      } else if (g.cnt == 1) {
-        piece_copy(g, g.code, 20);
-        g.cnt = 2;
-      } else {
-        piece_lit(g, 0xAC88ull, 2);
-        g.phase = PH_F_VALUE;
-      }
-      break;
-    case PH_F_VALUE: piece_lit(g, g.value, 8); g.phase = PH_F_SEQ; break;
-    case PH_F_SEQ: piece_copy(g, T + g.in_i_seq, 4); g.cnt = 0; g.phase = PH_F_HO; break;
-    case PH_F_HO:
-      piece_hash(g, g.ho, g.cnt);
-      g.cnt += 1;
-      if (g.cnt == 4) g.phase = PH_F_LOCK;
-      break;
-    case PH_F_LOCK: piece_copy(g, T + g.lock, 4); g.phase = PH_F_SH; break;
-    case PH_F_SH: piece_lit(g, g.shn, 4); g.phase = PH_DONE; break;
-    // ---- hashPrevouts / hashSequence inputs ----
-    case PH_P_IN: {
-      if (g.j == g.nin) {
-        g.phase = PH_DONE;
-        break;
-      }
-      piece_copy(g, T + g.ioff, 36);
-      uint32_t o = g.ioff + 36;
-      const uint32_t sl = get_varint(T, o);
-      g.ioff = o + sl + 4;
-      g.j += 1;
-      break;
-    }
-    case PH_S_IN: {
-      if (g.j == g.nin) {
-        g.phase = PH_DONE;
-        break;
-      }
-      uint32_t o = g.ioff + 36;
-      const uint32_t sl = get_varint(T, o);
-      piece_copy(g, T + o + sl, 4);
-      g.ioff = o + sl + 4;
-      g.j += 1;
-      break;
-    }
-    case PH_RANGE: piece_copy(g, g.code, g.code_len); g.phase = PH_DONE; break;
-    default: g.phase = PH_DONE; break;
-  }
-}
-
-HKV_DEV bool gen_more(Gen& g) {
-  while (g.rem == 0 && g.phase != PH_DONE) gen_advance(g);
-  return g.rem != 0;
-}
-HKV_DEV uint32_t gen_next(Gen& g) {
-  uint32_t b;
-  if (g.src) {
-    b = *g.src;
-    g.src += 1;
-  } else {
-    b = (uint32_t)g.lit & 0xFFu;
-    g.lit >>= 8;
-  }
-  g.rem -= 1;
-  return b;
-}
-
-// Block-extraction kernels (hkv_tx_hash_kernel, hkv_sighash_kernel,
-// hkv_std_input_kernel) take one-wave workgroups for up to HKV_XSMALL lanes
-// (a block: its lanes spread over 4x the CUs; configs[0] 696 -> 687 us,
-// configs[2] 736 -> 726 us) and WG-thread ones above (batches of blocks:
-// 64-thread groups measured 1-3% slower there; profiles/r02_variants_xtpb.log).
-// Their LDS slots keep the WG stride either way.
-#ifndef HKV_XSMALL
-#define HKV_XSMALL 16384
-#endif
-static inline uint32_t xtpb_for(size_t n) { return n <= HKV_XSMALL ? 64u : (uint32_t)WG; }
-
-// The next up to 4 message bytes, packed big-endian from the top of w;
-// returns how many (fewer than 4 only at the end of the message). Inside a
-// piece the 4 bytes come from 4 independent loads (or the literal's next
-// 32 bits) instead of 4 dependent load / store rounds; piece boundaries take
-// the byte path.
-HKV_DEV uint32_t gen_word(Gen& g, uint32_t& w) {
-  if (g.rem >= 4u) {
-    if (g.src) {
-      const uint8_t* s = g.src;
-      w = ((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) | ((uint32_t)s[2] << 8) | (uint32_t)s[3];
-      g.src += 4;
-    } else {
-      w = __builtin_bswap32((uint32_t)g.lit);
-      g.lit >>= 32;
-    }
-    g.rem -= 4u;
-    return 4u;
-  }
-  uint32_t n = 0;
-  w = 0;
-  for (int k = 0; k < 4; ++k) {
-    if (!gen_more(g)) break;
-    w |= gen_next(g) << (24 - 8 * k);
-    ++n;
-  }
-  return n;
-}
-
-// SHA-256 of the generator's message, block-synchronous over the wave: each
-// iteration every live lane writes its next 64 bytes (message, then 0x80,
-// zeros and the 64-bit length) into its LDS slot buf[word * WG + tid] and all
-// of them compress together. Call from wave-uniform control flow.
-HKV_DEV void sha256_stream(uint32_t h[8], Gen& g, bool live, uint32_t* buf) {
-  sha256_init(h);
-  const uint32_t tid = threadIdx.x;
-  // word at a time: 16 LDS word stores per block; 0x80 right after the last
-  // message byte; the length in words 14-15 of the block that has room
-  // (the byte-at-a-time form it replaced: extraction 188 -> 152 us on the
-  // configs[2] block, profiles/r02_variants.log)
-  uint32_t st = live ? 0u : 3u;  // 0 message, 1 padding (0x80 written), 3 done
-  uint64_t len = 0;
-  while (__any(st != 3u)) {
-    if (st != 3u) {
-      bool fits = st == 1u;  // a block after the 0x80 block always has room
-#pragma unroll 1
-      for (uint32_t k = 0; k < 16u; ++k) {
-        uint32_t v = 0;
-        if (st == 0u) {
-          const uint32_t nb = gen_word(g, v);
-          len += nb;
-          if (nb < 4u) {
-            v |= 0x80u << (24 - 8 * nb);
-            st = 1u;
-            fits = k < 14u;
-          }
-        }
-        buf[k * WG + tid] = v;
-      }
-      uint32_t w[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = buf[k * WG + tid];
-      const bool last = st == 1u && fits;
-      if (last) {
-        const uint64_t bits = len << 3;
-        w[14] = (uint32_t)(bits >> 32);
-        w[15] = (uint32_t)bits;
-      }
-      sha256_compress(h, w);
-      if (last) st = 3u;
-    }
-  }
-}
-
-// SHA-256d digest -> 8 words in digest byte order
-HKV_DEV void sha256d_finish(uint32_t out[8], const uint32_t h[8]) {
-  uint32_t d[8];
-  sha256_of_digest(d, h);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) out[k] = __builtin_bswap32(d[k]);
-}
-
-// ---------------------------------------------------------------------------
-// walkers over a validated tx
-// ---------------------------------------------------------------------------
-HKV_DEV void walk_input(const uint8_t* T, uint32_t ins, uint32_t i, uint32_t& in_off, uint32_t& ss_off,
-                        uint32_t& ss_len, uint32_t& seq_off) {
-  uint32_t off = ins;
-  for (uint32_t j = 0;; ++j) {
-    uint32_t o = off + 36;
-    const uint32_t sl = get_varint(T, o);
-    if (j == i) {
-      in_off = off;
-      ss_off = o;
-      ss_len = sl;
-      seq_off = o + sl;
-      return;
-    }
-    off = o + sl + 4;
-  }
-}
-HKV_DEV uint32_t walk_output(const uint8_t* T, uint32_t first, uint32_t k) {
-  uint32_t off = first;
-  for (uint32_t j = 0; j < k; ++j) {
-    uint32_t o = off + 8;
-    const uint32_t sl = get_varint(T, o);
-    off = o + sl;
-  }
-  return off;
-}
-HKV_DEV uint32_t walk_witness(const uint8_t* T, uint32_t wstart, uint32_t i) {
-  uint32_t off = wstart;
-  for (uint32_t j = 0; j < i; ++j) {
-    const uint32_t cnt = get_varint(T, off);
-    for (uint32_t c = 0; c < cnt; ++c) {
-      const uint32_t il = get_varint(T, off);
-      off += il;
-    }
-  }
-  return off;
-}
-
-// ---------------------------------------------------------------------------
-// 1. tx index
-// ---------------------------------------------------------------------------
-// bounds-checked parse of tx t's wire form into the first 8 words of its row
-HKV_DEV void tx_index_row(const uint8_t* __restrict__ txs, const uint32_t* __restrict__ tx_off, uint32_t t,
-                          uint32_t row[8]) {
-  bool ok = false;
-  {
-    const uint32_t st = tx_off[t], end = tx_off[t + 1];
-    ok = end >= st && end - st >= 10;
-    uint32_t off = st + 4, nin = 0, nout = 0;
-    bool seg = false;
-    if (ok && txs[off] == 0 && txs[off + 1] == 1) {
-      seg = true;
-      off += 2;
-    }
-    ok = ok && rd_varint(txs, off, end, nin);
-    const uint32_t ins = off;
-    for (uint32_t j = 0; ok && j < nin; ++j) {
-      uint32_t sl = 0;
-      ok = end - off >= 36;
-      off += ok ? 36 : 0;
-      ok = ok && rd_varint(txs, off, end, sl) && end - off >= 4 && end - off - 4 >= sl;
-      off += ok ? sl + 4 : 0;
-    }
-    ok = ok && rd_varint(txs, off, end, nout);
-    const uint32_t outs_first = off;
-    for (uint32_t k = 0; ok && k < nout; ++k) {
-      uint32_t sl = 0;
-      ok = end - off >= 8;
-      off += ok ? 8 : 0;
-      ok = ok && rd_varint(txs, off, end, sl) && end - off >= sl;
-      off += ok ? sl : 0;
-    }
-    const uint32_t outs_end = off;
-    for (uint32_t j = 0; ok && seg && j < nin; ++j) {
-      uint32_t cnt = 0;
-      ok = rd_varint(txs, off, end, cnt);
-      for (uint32_t c = 0; ok && c < cnt; ++c) {
-        uint32_t il = 0;
-        ok = rd_varint(txs, off, end, il) && end - off >= il;
-        off += ok ? il : 0;
-      }
-    }
-    ok = ok && end - off == 4;
-    row[TXT_FLAGS] = (ok ? TXF_OK : 0u) | (seg ? TXF_WITNESS : 0u);
-    row[TXT_INS] = ins;
-    row[TXT_NIN] = nin;
-    row[TXT_NOUT] = nout;
-    row[TXT_OUTS_FIRST] = outs_first;
-    row[TXT_OUTS_END] = outs_end;
-    row[TXT_LOCK] = off;
-    row[TXT_START] = st;
-  }
-}
 
 __global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restrict__ txs,
                                                           const uint32_t* __restrict__ tx_off, uint32_t n_tx,
@@ -610,72 +86,6 @@ __global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restri
     const int slot = which == 0 ? TXT_HP : (which == 1 ? TXT_HS : TXT_HO);
 #pragma unroll
     for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + slot + k] = d[k];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// shared per-job setup: everything a legacy / BIP143 preimage needs
-// ---------------------------------------------------------------------------
-struct JobCtx {
-  uint32_t start, nin, nout, ins, outs_first, lock;
-  uint32_t i, sh, shn, flags;
-  uint32_t in_i, in_i_seq, single_off;
-  bool forkid_form;   // BIP143 preimage
-  bool one;           // legacy SINGLE with i >= #outputs: sign the integer one
-  bool single_hash;   // BIP143 SINGLE with i < #outputs: per-job hashOutputs
-};
-
-HKV_DEV void job_setup(JobCtx& c, const uint8_t* T, const uint32_t* row, uint32_t i, uint32_t sh, bool forkid_form,
-                       int32_t forkid) {
-  c.start = row[TXT_START];
-  c.nin = row[TXT_NIN];
-  c.nout = row[TXT_NOUT];
-  c.ins = row[TXT_INS];
-  c.outs_first = row[TXT_OUTS_FIRST];
-  c.lock = row[TXT_LOCK];
-  c.i = i;
-  c.sh = sh;
-  // txSigHash on a fork-id network dispatches FORKID-flagged types to the BIP143 form
-  c.forkid_form = forkid_form || (forkid >= 0 && (sh & 0x40u));
-  c.shn = (c.forkid_form && forkid >= 0) ? (sh | ((uint32_t)forkid << 8)) : sh;
-  const uint32_t base = sh & 0x1Fu;
-  const bool none = base == 2u, single = base == 3u;
-  c.flags = ((sh & 0x80u) ? GF_ACP : 0u) | ((!none && !single) ? GF_ALL : 0u) | (none ? GF_NONE : 0u) |
-            (single ? GF_SINGLE : 0u);
-  uint32_t ss_off, ss_len;
-  walk_input(T, c.ins, i, c.in_i, ss_off, ss_len, c.in_i_seq);
-  c.one = !c.forkid_form && single && i >= c.nout;
-  c.single_hash = c.forkid_form && single && i < c.nout;
-  c.single_off = (single && i < c.nout) ? walk_output(T, c.outs_first, i) : 0u;
-}
-
-// main-preimage generator for a job; code = scriptCode bytes (for the
-// P2WPKH form: the 20-byte program, flag GF_P2WPKH)
-HKV_DEV void gen_job(Gen& g, const JobCtx& c, const uint8_t* T, const uint32_t* row, const uint8_t* code,
-                     uint32_t code_len, bool p2wpkh_code, uint64_t value, const uint32_t* single_ho) {
-  gen_clear(g);
-  g.T = T;
-  g.start = c.start; g.nin = c.nin; g.nout = c.nout; g.ins = c.ins; g.outs_first = c.outs_first; g.lock = c.lock;
-  g.i = c.i; g.shn = c.shn; g.flags = c.flags;
-  g.in_i = c.in_i; g.in_i_seq = c.in_i_seq; g.single_off = c.single_off;
-  g.code = code; g.code_len = code_len; g.code_out = code_len; g.value = value;
-  if (c.forkid_form) {
-    if (p2wpkh_code) {
-      g.flags |= GF_P2WPKH;
-      g.code_len = 25;
-    }
-    const bool acp = (c.flags & GF_ACP) != 0;
-    g.hp = acp ? nullptr : row + TXT_HP;
-    g.hs = (acp || !(c.flags & GF_ALL)) ? nullptr : row + TXT_HS;
-    g.ho = (c.flags & GF_ALL) ? row + TXT_HO : (c.single_hash ? single_ho : nullptr);
-    g.phase = PH_F_VER;
-  } else {
-    uint32_t n_sep = 0;
-    if (script_scan(code, code_len, n_sep) && n_sep) {
-      g.flags |= GF_STRIP;
-      g.code_out = code_len - n_sep;
-    }
-    g.phase = PH_L_VER;
   }
 }
 
@@ -743,144 +153,6 @@ __global__ void __launch_bounds__(WG) hkv_sighash_kernel(const uint8_t* __restri
   }
 }
 
-// ---------------------------------------------------------------------------
-// 3. standard inputs -> verify records
-// ---------------------------------------------------------------------------
-// secp256k1_der_read_len
-HKV_DEV bool der_read_len(const uint8_t* p, uint32_t& off, uint32_t end, uint32_t& len) {
-  if (off >= end) return false;
-  const uint32_t b1 = p[off++];
-  if (b1 == 0xFFu) return false;
-  if ((b1 & 0x80u) == 0) {
-    len = b1;
-    return true;
-  }
-  const uint32_t lenleft = b1 & 0x7Fu;
-  if (lenleft == 0) return false;          // indefinite length
-  if (lenleft > end - off) return false;
-  if (p[off] == 0) return false;           // not the shortest encoding
-  if (lenleft > 8) return false;
-  uint64_t v = 0;
-  for (uint32_t k = 0; k < lenleft; ++k) v = (v << 8) | p[off++];
-  if (v > (uint64_t)(end - off)) return false;
-  if (v < 128) return false;
-  len = (uint32_t)v;
-  return true;
-}
-// secp256k1_der_parse_integer: overflow (negative, > 32 bytes, >= n) -> 0
-HKV_DEV bool der_parse_int(const uint8_t* p, uint32_t& off, uint32_t end, uint32_t r[8]) {
-  if (off >= end || p[off] != 0x02u) return false;
-  ++off;
-  uint32_t rlen = 0;
-  if (!der_read_len(p, off, end, rlen)) return false;
-  if (rlen == 0 || rlen > end - off) return false;
-  const uint32_t b0 = p[off], b1 = rlen > 1 ? p[off + 1] : 0u;
-  if (b0 == 0x00u && rlen > 1 && (b1 & 0x80u) == 0) return false;
-  if (b0 == 0xFFu && rlen > 1 && (b1 & 0x80u) == 0x80u) return false;
-  bool overflow = (b0 & 0x80u) != 0;
-  if (b0 == 0) {
-    ++off;
-    --rlen;
-  }
-  if (rlen > 32) overflow = true;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r[k] = 0;
-  if (!overflow) {
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      if ((uint32_t)q < rlen) r[q >> 2] |= (uint32_t)p[off + rlen - 1 - q] << (8 * (q & 3));
-    }
-    if (!u256_lt(r, SC_N)) overflow = true;
-  }
-  if (overflow) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = 0;
-  }
-  off += rlen;
-  return true;
-}
-HKV_DEV bool der_parse_sig(const uint8_t* p, uint32_t off, uint32_t end, uint32_t r[8], uint32_t s[8]) {
-  if (off >= end || p[off] != 0x30u) return false;
-  ++off;
-  uint32_t len = 0;
-  if (!der_read_len(p, off, end, len)) return false;
-  if (len != end - off) return false;
-  if (!der_parse_int(p, off, end, r)) return false;
-  if (!der_parse_int(p, off, end, s)) return false;
-  return off == end;
-}
-// haskoin-core decodeTxSig: hashtype byte (known base type; FORKID only on a
-// fork-id network), then decodeStrictSig = DER parse + r, s != 0 + low S.
-HKV_DEV bool decode_tx_sig(const uint8_t* p, uint32_t off, uint32_t len, int32_t forkid, uint32_t r[8], uint32_t s[8],
-                           uint32_t& sh) {
-  if (len < 1) return false;
-  sh = p[off + len - 1];
-  const uint32_t base = sh & 0x1Fu;
-  if (!(base >= 1u && base <= 3u && !(forkid < 0 && (sh & 0x40u)))) return false;
-  if (!der_parse_sig(p, off, off + len - 1, r, s)) return false;
-  return !u256_is_zero(r) && !u256_is_zero(s) && !u256_lt(SC_HALF_N, s);
-}
-
-// one data push (opcodes 1..78) at off within [off, end): data range
-HKV_DEV bool read_push(const uint8_t* p, uint32_t& off, uint32_t end, uint32_t& d_off, uint32_t& d_len) {
-  if (off >= end) return false;
-  const uint32_t op = p[off];
-  uint32_t hdr, len;
-  if (op >= 1u && op <= 75u) {
-    hdr = 1;
-    len = op;
-  } else if (op == 0x4Cu) {
-    if (end - off < 2) return false;
-    hdr = 2;
-    len = p[off + 1];
-  } else if (op == 0x4Du) {
-    if (end - off < 3) return false;
-    hdr = 3;
-    len = p[off + 1] | (p[off + 2] << 8);
-  } else if (op == 0x4Eu) {
-    if (end - off < 5) return false;
-    hdr = 5;
-    len = p[off + 1] | (p[off + 2] << 8) | (p[off + 3] << 16) | ((uint32_t)p[off + 4] << 24);
-  } else {
-    return false;
-  }
-  if ((uint64_t)hdr + len > (uint64_t)(end - off)) return false;
-  d_off = off + hdr;
-  d_len = len;
-  off += hdr + len;
-  return true;
-}
-
-// haskoin PubKeyI encoding: 02/03 + 32 bytes or 04 + 64 bytes
-HKV_DEV bool pubkey_bytes_ok(const uint8_t* p, uint32_t len) {
-  return (len == 33u && (p[0] == 2u || p[0] == 3u)) || (len == 65u && p[0] == 4u);
-}
-// direct-push P2PK script (21 <33> ac / 41 <65> ac)
-HKV_DEV bool is_p2pk(const uint8_t* sc, uint32_t L) {
-  return ((L == 35u && sc[0] == 0x21u) || (L == 67u && sc[0] == 0x41u)) && sc[L - 1] == 0xACu;
-}
-HKV_DEV bool is_p2pkh(const uint8_t* sc, uint32_t L) {
-  return L == 25u && sc[0] == 0x76u && sc[1] == 0xA9u && sc[2] == 0x14u && sc[23] == 0x88u && sc[24] == 0xACu;
-}
-// 20-byte hash in memory == RIPEMD-160 words / 32-byte hash == SHA-256 state
-HKV_DEV bool eq_h160(const uint8_t* p, const uint32_t rip[5]) {
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < 5; ++k)
-    ok = ok && (uint32_t)(p[4 * k] | (p[4 * k + 1] << 8) | (p[4 * k + 2] << 16) | ((uint32_t)p[4 * k + 3] << 24)) == rip[k];
-  return ok;
-}
-HKV_DEV bool eq_sha256(const uint8_t* p, const uint32_t h[8]) {
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-    ok = ok && (((uint32_t)p[4 * k] << 24) | (p[4 * k + 1] << 16) | (p[4 * k + 2] << 8) | p[4 * k + 3]) == h[k];
-  return ok;
-}
-
-// Single-signature templates (haskoin verifyStdInput): P2PK, P2PKH, P2WPKH;
-// P2SH around P2PK / P2PKH / P2WPKH / P2WSH; P2WSH (native or P2SH-nested)
-// around P2PK / P2PKH. Multisig inputs: hkv_ms_* (section 4).
 __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
                                                            const uint32_t* __restrict__ txt,
                                                            const uint8_t* __restrict__ scripts, uint32_t scripts_len,
@@ -888,242 +160,13 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
                                                            int32_t forkid, uint8_t* __restrict__ recs) {
   __shared__ uint32_t buf[16 * WG];
   const uint32_t jx = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in_range = jx < n;
-  bool ok = false;
-  const uint32_t* row = txt;
-  const uint8_t* spk = scripts;
-  uint32_t sig_off = 0, sig_len = 0, pub_len = 0, sh = 0, input = 0;
-  const uint8_t* pub = txs;
-  uint64_t value = 0;
-  // what the checks and the sighash need
-  const uint8_t* code = scripts;  // sighash scriptCode (P2WPKH form: the 20-byte program)
-  uint32_t code_len = 0;
-  bool segwit = false, p2wpkh = false;
-  const uint8_t* kh = scripts;    // HASH160(pubkey) must equal these 20 bytes (has_kh)
-  const uint8_t* rd = txs;        // P2SH: HASH160(redeem script) == spk[2..22] (has_rd)
-  uint32_t rd_len = 0;
-  const uint8_t* ws = txs;        // P2WSH: SHA-256(witness script) == wprog (has_ws)
-  uint32_t ws_len = 0;
-  const uint8_t* wprog = scripts;
-  bool has_kh = false, has_rd = false, has_ws = false;
-  uint32_t r[8], s[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r[k] = s[k] = 0;
-  if (in_range) {
-    const hkv_input_job jb = jobs[jx];
-    input = jb.input;
-    value = jb.value;
-    ok = jb.tx < n_tx && jb.script_off <= scripts_len && scripts_len - jb.script_off >= jb.script_len;
-    if (ok) {
-      row = txt + (size_t)jb.tx * TXT_WORDS;
-      ok = (row[TXT_FLAGS] & TXF_OK) && jb.input < row[TXT_NIN];
-    }
-    if (ok) {
-      spk = scripts + jb.script_off;
-      const uint32_t L = jb.script_len;
-      uint32_t in_off, ss_off, ss_len, seq_off;
-      walk_input(txs, row[TXT_INS], jb.input, in_off, ss_off, ss_len, seq_off);
-      const uint32_t ss_end = ss_off + ss_len;
-      uint32_t c = ss_off, pub_off = 0;
-      // witness program to open: 1 P2WPKH [sig, pub], 2 P2WSH [stack.., ws]
-      uint32_t open_wit = 0;
-      if (is_p2pk(spk, L)) {  // scriptSig = <sig>; pubkey from the prevout
-        ok = read_push(txs, c, ss_end, sig_off, sig_len) && c == ss_end;
-        pub = spk + 1;
-        pub_len = L - 2;
-        code = spk;
-        code_len = L;
-      } else if (is_p2pkh(spk, L)) {  // scriptSig = <sig> <pubkey>
-        ok = read_push(txs, c, ss_end, sig_off, sig_len) && read_push(txs, c, ss_end, pub_off, pub_len) &&
-             c == ss_end;
-        pub = txs + pub_off;
-        kh = spk + 3;
-        has_kh = true;
-        code = spk;
-        code_len = 25;
-      } else if (L == 22u && spk[0] == 0x00u && spk[1] == 0x14u) {  // P2WPKH: empty scriptSig
-        ok = ss_len == 0;
-        code = kh = spk + 2;
-        has_kh = true;
-        open_wit = 1;
-      } else if (L == 34u && spk[0] == 0x00u && spk[1] == 0x20u) {  // P2WSH: empty scriptSig
-        ok = ss_len == 0;
-        wprog = spk + 2;
-        open_wit = 2;
-      } else if (L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u) {
-        // P2SH: every op a push; the last one is the redeem script
-        uint32_t np = 0, o0 = 0, l0 = 0, o1 = 0, l1 = 0, ol = 0, ll = 0;
-        while (ok && c < ss_end) {
-          uint32_t d_off = 0, d_len = 0;
-          ok = read_push(txs, c, ss_end, d_off, d_len);
-          if (np == 0) { o0 = d_off; l0 = d_len; }
-          if (np == 1) { o1 = d_off; l1 = d_len; }
-          ol = d_off;
-          ll = d_len;
-          ++np;
-        }
-        ok = ok && np >= 1;
-        rd = txs + ol;
-        rd_len = ll;
-        has_rd = true;
-        if (ok) {
-          if (ll == 22u && rd[0] == 0u && rd[1] == 0x14u) {  // P2SH-P2WPKH
-            ok = np == 1;
-            code = kh = rd + 2;
-            has_kh = true;
-            open_wit = 1;
-          } else if (ll == 34u && rd[0] == 0u && rd[1] == 0x20u) {  // P2SH-P2WSH
-            ok = np == 1;
-            wprog = rd + 2;
-            open_wit = 2;
-          } else if (is_p2pk(rd, ll)) {  // P2SH-P2PK: <sig> <redeem>
-            ok = np == 2;
-            sig_off = o0; sig_len = l0;
-            pub = rd + 1;
-            pub_len = ll - 2;
-            code = rd;
-            code_len = ll;
-          } else if (is_p2pkh(rd, ll)) {  // P2SH-P2PKH: <sig> <pubkey> <redeem>
-            ok = np == 3;
-            sig_off = o0; sig_len = l0;
-            pub = txs + o1;
-            pub_len = l1;
-            kh = rd + 3;
-            has_kh = true;
-            code = rd;
-            code_len = 25;
-          } else {
-            ok = false;  // multisig redeem scripts: hkv_ms_*; anything else is not standard
-          }
-        }
-      } else {
-        ok = false;
-      }
-      if (ok && open_wit) {
-        ok = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
-        uint32_t w = ok ? walk_witness(txs, row[TXT_OUTS_END], jb.input) : 0u;
-        const uint32_t cnt = ok ? get_varint(txs, w) : 0u;
-        if (open_wit == 1) {  // [sig, pubkey]
-          ok = ok && cnt == 2u;
-          if (ok) {
-            sig_len = get_varint(txs, w);
-            sig_off = w;
-            w += sig_len;
-            pub_len = get_varint(txs, w);
-            pub = txs + w;
-          }
-          segwit = p2wpkh = true;
-        } else {  // [sig, ws] (P2PK) or [sig, pubkey, ws] (P2PKH)
-          ok = ok && (cnt == 2u || cnt == 3u);
-          if (ok) {
-            sig_len = get_varint(txs, w);
-            sig_off = w;
-            w += sig_len;
-            uint32_t l1 = 0, o1 = 0;
-            if (cnt == 3u) {
-              l1 = get_varint(txs, w);
-              o1 = w;
-              w += l1;
-            }
-            ws_len = get_varint(txs, w);
-            ws = txs + w;
-            has_ws = true;
-            if (cnt == 2u && is_p2pk(ws, ws_len)) {
-              pub = ws + 1;
-              pub_len = ws_len - 2;
-            } else if (cnt == 3u && is_p2pkh(ws, ws_len)) {
-              pub = txs + o1;
-              pub_len = l1;
-              kh = ws + 3;
-              has_kh = true;
-            } else {
-              ok = false;  // P2WSH multisig: hkv_ms_*
-            }
-            code = ws;
-            code_len = ws_len;
-          }
-          segwit = true;
-        }
-      }
-    }
-    if (ok) ok = decode_tx_sig(txs, sig_off, sig_len, forkid, r, s, sh);
-    if (ok) ok = pubkey_bytes_ok(pub, pub_len);
-  }
-  Gen g;
-  uint32_t h[8], d[8];
-  // HASH160(pubkey) == the key hash (P2PKH, P2WPKH and their wrapped forms)
-  const bool need_h160 = ok && has_kh;
-  if (__any(need_h160)) {
-    gen_clear(g);
-    g.code = pub; g.code_len = pub_len; g.phase = PH_RANGE;
-    sha256_stream(h, g, need_h160, buf);
-    uint32_t rip[5];
-    ripemd160_of_digest(rip, h);
-    if (need_h160) ok = ok && eq_h160(kh, rip);
-  }
-  // P2SH: HASH160(redeem script) == the script hash
-  const bool need_rd = ok && has_rd;
-  if (__any(need_rd)) {
-    gen_clear(g);
-    g.code = rd; g.code_len = rd_len; g.phase = PH_RANGE;
-    sha256_stream(h, g, need_rd, buf);
-    uint32_t rip[5];
-    ripemd160_of_digest(rip, h);
-    if (need_rd) ok = ok && eq_h160(spk + 2, rip);
-  }
-  // P2WSH: SHA-256(witness script) == the 32-byte program
-  const bool need_ws = ok && has_ws;
-  if (__any(need_ws)) {
-    gen_clear(g);
-    g.code = ws; g.code_len = ws_len; g.phase = PH_RANGE;
-    sha256_stream(h, g, need_ws, buf);
-    if (need_ws) ok = ok && eq_sha256(wprog, h);
-  }
-  // sighash: legacy txSigHash over the scriptCode (prevout or redeem script),
-  // or txSigHashForkId (BIP143) over 76 a9 14 <h20> 88 ac (P2WPKH) / the
-  // witness script (P2WSH)
-  JobCtx c;
-  c.forkid_form = false; c.one = false; c.single_hash = false;
-  if (ok) job_setup(c, txs, row, input, sh, segwit, forkid);
-  uint8_t* rec = recs + (size_t)jx * REC_SIZE;
-  uint32_t* r32 = reinterpret_cast<uint32_t*>(rec);
-  const bool need_single = ok && c.single_hash;
-  if (__any(need_single)) {
-    gen_clear(g);
-    g.T = txs; g.ooff = c.single_off; g.ocnt = 1; g.ret = PH_DONE; g.phase = PH_O_VAL;
-    sha256_stream(h, g, need_single, buf);
-    sha256d_finish(d, h);
-    if (need_single) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) r32[k] = d[k];  // scratch: record bytes 0..31
-    }
-  }
-  const bool live = ok && !c.one;
-  if (!live) gen_clear(g);
-  else gen_job(g, c, txs, row, code, p2wpkh ? 20u : code_len, p2wpkh, value, r32);
-  sha256_stream(h, g, live, buf);
-  sha256d_finish(d, h);
-  if (!in_range) return;
-  // record: msg32 | r | s | pklen | pubkey | 0 (all zero when a check failed)
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    r32[k] = !ok ? 0u : (live ? d[k] : (k == 0 ? 1u : 0u));
-    r32[8 + k] = ok ? __builtin_bswap32(r[7 - k]) : 0u;
-    r32[16 + k] = ok ? __builtin_bswap32(s[7 - k]) : 0u;
-  }
-#pragma unroll
-  for (int w = 0; w < 18; ++w) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int q = 4 * w + b;  // byte 96 + q of the record
-      uint32_t byte = 0;
-      if (q == 0) byte = pub_len;
-      else if ((uint32_t)(q - 1) < pub_len && q - 1 < 65) byte = pub[q - 1];
-      v |= byte << (8 * b);
-    }
-    r32[24 + w] = ok ? v : 0u;
-  }
+  StdIn x;
+  std_parse(x, txs, n_tx, txt, scripts, scripts_len, jobs, jx, n, forkid);
+  uint32_t* r32 = reinterpret_cast<uint32_t*>(recs + (size_t)jx * REC_SIZE);
+  uint32_t d[8];
+  const bool live = std_hash(x, txs, forkid, r32, buf, d);
+  if (jx >= n) return;
+  std_write_record(r32, x, live, d);
 }
 
 // ---------------------------------------------------------------------------
