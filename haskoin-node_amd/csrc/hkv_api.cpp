@@ -366,10 +366,12 @@ bool txs_ok(const hkv_txs* t) {
          t->n_tx < 0xFFFFFF00u;
 }
 
-int enqueue_tx_index(DevCtx& d, const hkv_txs* dt, hipStream_t st) {
+// the tx index rows, with the BIP143 per-tx hashes unless bip143 is false
+// (the fused small-batch std-input launch computes them per input)
+int enqueue_tx_index(DevCtx& d, const hkv_txs* dt, hipStream_t st, bool bip143 = true) {
   int rc = grow(reinterpret_cast<void**>(&d.txt), &d.txt_cap, (size_t)dt->n_tx * hkv::TXT_WORDS * 4, "hipMalloc(txt)");
   if (rc) return rc;
-  HKV_TRY(hkv::launch_tx_index(dt->bytes, dt->offsets, dt->n_tx, 1u, d.txt, st), "tx index launch");
+  HKV_TRY(hkv::launch_tx_index(dt->bytes, dt->offsets, dt->n_tx, bip143 ? 1u : 0u, d.txt, st), "tx index launch");
   return HKV_OK;
 }
 
@@ -450,7 +452,7 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   // it, off the block's critical path); larger ones: the extraction kernel,
   // then the record verify
   const bool fused = split_batch(d, n);
-  int rc = fused ? enqueue_tx_index(d, dt, st) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  int rc = fused ? enqueue_tx_index(d, dt, st, false) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, st);
   if (rc) return rc;
   rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
@@ -497,6 +499,10 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
   uint8_t* keyrec = cand + n_cand * hkv::REC_SIZE;
   uint32_t* kbits = static_cast<uint32_t*>(d.ms[5]);
+  if (fused) {  // the multisig sighashes read the BIP143 per-tx hashes from the index rows
+    rc = enqueue_tx_index(d, dt, st, true);
+    if (rc) return rc;
+  }
   HKV_TRY(hkv::launch_ms_emit(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
                               desc, off, cand, keyrec, st),
           "multisig emit launch");

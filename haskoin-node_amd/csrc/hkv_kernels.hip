@@ -973,7 +973,10 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
         uint32_t* r32 = recs + (size_t)(ln < PAIR_SIGS && i < n ? i : 0) * REC_WORDS;
         if (ln >= PAIR_SIGS) x.ok = false;
         uint32_t d[8];
-        const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d);  // (writes r32 only when x.ok)
+        // (r32 is scratch until the record is written: words 0-7 for a BIP143
+        // SINGLE hashOutputs, 8-31 for the tx's BIP143 hashes, which the
+        // fused launch computes per input instead of an index-kernel pass)
+        const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8);
         if (ln < PAIR_SIGS) {
           if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
           uint32_t w[8];

@@ -575,9 +575,12 @@ HKV_DEV void job_setup(JobCtx& c, const uint8_t* T, const uint32_t* row, uint32_
 }
 
 // main-preimage generator for a job; code = scriptCode bytes (for the
-// P2WPKH form: the 20-byte program, flag GF_P2WPKH)
+// P2WPKH form: the 20-byte program, flag GF_P2WPKH); h3: the tx's BIP143
+// hashPrevouts | hashSequence | hashOutputs (24 words; null: the index row's)
 HKV_DEV void gen_job(Gen& g, const JobCtx& c, const uint8_t* T, const uint32_t* row, const uint8_t* code,
-                     uint32_t code_len, bool p2wpkh_code, uint64_t value, const uint32_t* single_ho) {
+                     uint32_t code_len, bool p2wpkh_code, uint64_t value, const uint32_t* single_ho,
+                     const uint32_t* h3 = nullptr) {
+  if (h3 == nullptr) h3 = row + TXT_HP;
   gen_clear(g);
   g.T = T;
   g.start = c.start; g.nin = c.nin; g.nout = c.nout; g.ins = c.ins; g.outs_first = c.outs_first; g.lock = c.lock;
@@ -590,9 +593,9 @@ HKV_DEV void gen_job(Gen& g, const JobCtx& c, const uint8_t* T, const uint32_t* 
       g.code_len = 25;
     }
     const bool acp = (c.flags & GF_ACP) != 0;
-    g.hp = acp ? nullptr : row + TXT_HP;
-    g.hs = (acp || !(c.flags & GF_ALL)) ? nullptr : row + TXT_HS;
-    g.ho = (c.flags & GF_ALL) ? row + TXT_HO : (c.single_hash ? single_ho : nullptr);
+    g.hp = acp ? nullptr : h3;
+    g.hs = (acp || !(c.flags & GF_ALL)) ? nullptr : h3 + 8;
+    g.ho = (c.flags & GF_ALL) ? h3 + 16 : (c.single_hash ? single_ho : nullptr);
     g.phase = PH_F_VER;
   } else {
     uint32_t n_sep = 0;
@@ -942,13 +945,42 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
   for (int k = 0; k < 8; ++k) { x.r[k] = r[k]; x.s[k] = s[k]; }
 }
 
+// the three BIP143 per-tx hashes of row's tx into h3 (hashPrevouts |
+// hashSequence | hashOutputs) for the lanes that need them (block-synchronous)
+HKV_DEV void bip143_tx_hashes(const uint8_t* __restrict__ txs, const uint32_t* row, bool need, uint32_t* h3,
+                              uint32_t* buf) {
+#pragma unroll 1
+  for (int which = 0; which < 3; ++which) {
+    Gen g;
+    uint32_t h[8], d[8];
+    gen_clear(g);
+    g.T = txs;
+    if (need) {
+      if (which == 2) {  // hashOutputs (each output re-serialised canonically)
+        g.ooff = row[TXT_OUTS_FIRST]; g.ocnt = row[TXT_NOUT]; g.ret = PH_DONE; g.phase = PH_O_VAL;
+      } else {
+        g.nin = row[TXT_NIN]; g.ioff = row[TXT_INS]; g.j = 0; g.phase = which == 0 ? PH_P_IN : PH_S_IN;
+      }
+    }
+    sha256_stream(h, g, need, buf);
+    sha256d_finish(d, h);
+    if (need) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h3[8 * which + k] = d[k];
+    }
+  }
+}
+
 // Part B: the HASH160 / SHA-256 script checks and the sighash (updates x.ok).
 // Call from wave-uniform control flow (block-synchronous SHA-256 streams
 // through buf[16 * WG]). single_ho: 8 scratch words of the lane (BIP143
-// SINGLE parks its hashOutputs there). Returns whether d holds the sighash;
-// false with x.ok means the legacy SINGLE bug (the message is the integer 1).
+// SINGLE parks its hashOutputs there). h3: null when the index rows carry the
+// BIP143 per-tx hashes (hkv_tx_hash_kernel), else 24 scratch words of the
+// lane, where they are computed for this input's tx. Returns whether d holds
+// the sighash; false with x.ok means the legacy SINGLE bug (the message is
+// the integer 1).
 HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid, uint32_t* single_ho, uint32_t* buf,
-                      uint32_t d[8]) {
+                      uint32_t d[8], uint32_t* h3 = nullptr) {
   bool ok = x.ok;
   const uint32_t* row = x.row;
   const uint8_t* spk = x.spk;
@@ -1009,8 +1041,12 @@ HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid,
     }
   }
   const bool live = ok && !c.one;
+  if (h3 != nullptr) {
+    const bool need_tx = live && c.forkid_form;
+    if (__any(need_tx)) bip143_tx_hashes(txs, row, need_tx, h3, buf);
+  }
   if (!live) gen_clear(g);
-  else gen_job(g, c, txs, row, code, p2wpkh ? 20u : code_len, p2wpkh, value, r32);
+  else gen_job(g, c, txs, row, code, p2wpkh ? 20u : code_len, p2wpkh, value, r32, h3);
   sha256_stream(h, g, live, buf);
   sha256d_finish(d, h);
   x.ok = ok;
