@@ -366,18 +366,24 @@ bool txs_ok(const hkv_txs* t) {
          t->n_tx < 0xFFFFFF00u;
 }
 
-// the tx index rows, with the BIP143 per-tx hashes unless bip143 is false
-// (the fused small-batch std-input launch computes them per input)
-int enqueue_tx_index(DevCtx& d, const hkv_txs* dt, hipStream_t st, bool bip143 = true) {
+// the tx index rows, with the BIP143 per-tx hashes of the txs that may need
+// them (hkv::TX_HASHES_*: none — the fused small-batch std-input launch
+// computes them per input —, every tx — the sighash API, whose jobs choose
+// the BIP143 form freely —, or, for standard inputs, what the network allows)
+int enqueue_tx_index(DevCtx& d, const hkv_txs* dt, hipStream_t st, uint32_t hashes = hkv::TX_HASHES_ALL) {
   int rc = grow(reinterpret_cast<void**>(&d.txt), &d.txt_cap, (size_t)dt->n_tx * hkv::TXT_WORDS * 4, "hipMalloc(txt)");
   if (rc) return rc;
-  HKV_TRY(hkv::launch_tx_index(dt->bytes, dt->offsets, dt->n_tx, bip143 ? 1u : 0u, d.txt, st), "tx index launch");
+  HKV_TRY(hkv::launch_tx_index(dt->bytes, dt->offsets, dt->n_tx, hashes, d.txt, st), "tx index launch");
   return HKV_OK;
 }
+// verifyStdInput signs with BIP143 only for witness programs (then the tx
+// carries witness data, or the input fails) unless a fork id is in force,
+// where every FORKID-flagged signature does
+uint32_t std_tx_hashes(int32_t forkid) { return forkid >= 0 ? hkv::TX_HASHES_ALL : hkv::TX_HASHES_WITNESS; }
 
 int enqueue_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
                        void* recs, hipStream_t st) {
-  int rc = enqueue_tx_index(d, dt, st);
+  int rc = enqueue_tx_index(d, dt, st, std_tx_hashes(forkid));
   if (rc) return rc;
   HKV_TRY(hkv::launch_std_inputs(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
                                  static_cast<uint8_t*>(recs), st),
@@ -452,7 +458,7 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   // it, off the block's critical path); larger ones: the extraction kernel,
   // then the record verify
   const bool fused = split_batch(d, n);
-  int rc = fused ? enqueue_tx_index(d, dt, st, false) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  int rc = fused ? enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, st);
   if (rc) return rc;
   rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
@@ -500,7 +506,7 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   uint8_t* keyrec = cand + n_cand * hkv::REC_SIZE;
   uint32_t* kbits = static_cast<uint32_t*>(d.ms[5]);
   if (fused) {  // the multisig sighashes read the BIP143 per-tx hashes from the index rows
-    rc = enqueue_tx_index(d, dt, st, true);
+    rc = enqueue_tx_index(d, dt, st, std_tx_hashes(forkid));
     if (rc) return rc;
   }
   HKV_TRY(hkv::launch_ms_emit(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,

@@ -50,7 +50,7 @@ hipError_t launch_gen_keys(uint64_t seed, uint32_t n, uint8_t* priv, uint8_t* pu
 hipError_t launch_gen_sign(uint64_t seed, uint32_t n, const uint8_t* priv, const uint32_t* key_idx,
                            const uint8_t* msg, uint32_t msg_stride, uint8_t* sig, hipStream_t st);
 // hkv_sighash.hip
-hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t want_bip143,
+hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t hashes,
                            uint32_t* txt, hipStream_t st);
 hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_sighash_job* jobs, uint32_t n, int32_t forkid, uint8_t* out,

@@ -143,6 +143,8 @@ enum : int {
   TXT_WORDS = 32,
 };
 constexpr uint32_t TXF_OK = 1u, TXF_WITNESS = 2u;
+// which txs the index pass computes the BIP143 per-tx hashes for
+enum : uint32_t { TX_HASHES_NONE = 0, TX_HASHES_ALL = 1, TX_HASHES_WITNESS = 2 };
 
 // minimum waves per SIMD the ecmult kernel's register allocation targets
 #ifndef HKV_ECMULT_WAVES

@@ -56,9 +56,11 @@ __global__ void __launch_bounds__(WG) hkv_tx_index_kernel(const uint8_t* __restr
 // other (a block's index is latency-bound: one wave per 64 txs).
 // Each lane parses its tx itself (the three blockIdx.y lanes of a tx repeat
 // the cheap walk; y = 0 writes the row), so the index costs no launch of its own.
+// witness_only: hash only the txs with witness data (the others' rows keep
+// stale hash words, which no standard input on a network without a fork id reads)
 __global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restrict__ txs,
                                                          const uint32_t* __restrict__ tx_off, uint32_t n_tx,
-                                                         uint32_t* __restrict__ txt) {
+                                                         uint32_t witness_only, uint32_t* __restrict__ txt) {
   __shared__ uint32_t buf[16 * WG];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t which = blockIdx.y;  // 0 prevouts, 1 sequences, 2 outputs
@@ -70,7 +72,7 @@ __global__ void __launch_bounds__(WG) hkv_tx_hash_kernel(const uint8_t* __restri
       for (int k = 0; k < 8; ++k) txt[(size_t)t * TXT_WORDS + k] = row[k];
     }
   }
-  const bool go = t < n_tx && (row[TXT_FLAGS] & TXF_OK);
+  const bool go = t < n_tx && (row[TXT_FLAGS] & TXF_OK) && (!witness_only || (row[TXT_FLAGS] & TXF_WITNESS));
   Gen g;
   uint32_t h[8], d[8];
   gen_clear(g);
@@ -577,12 +579,12 @@ namespace hkv {
 
 static inline uint32_t blocks_for(size_t n) { return (uint32_t)((n + WG - 1) / WG); }
 
-hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t want_bip143,
+hipError_t launch_tx_index(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t hashes,
                            uint32_t* txt, hipStream_t st) {
   if (n_tx == 0) return hipSuccess;
-  if (want_bip143)
+  if (hashes != TX_HASHES_NONE)
     hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3((n_tx + xtpb_for(n_tx) - 1) / xtpb_for(n_tx), 3), dim3(xtpb_for(n_tx)), 0, st,
-                       txs, tx_off, n_tx, txt);
+                       txs, tx_off, n_tx, hashes == TX_HASHES_WITNESS ? 1u : 0u, txt);
   else
     hipLaunchKernelGGL(hkv_tx_index_kernel, dim3(blocks_for(n_tx)), dim3(WG), 0, st, txs, tx_off, n_tx, txt);
   return hipGetLastError();

@@ -39,22 +39,30 @@ BATCH_INV = 16       # signatures per s^-1 (hkv_layout.h)
 YFREE = True         # full-grid batches verify y-free (hkv_layout.h HKV_YFREE)
 
 
-def ecmult_products() -> int:
+def ecmult_products(qw: int = QW, beta_per_lookup: bool = False) -> int:
     """The ecmult stage: hkv_ecmult_kernel, plus (y-free) the finish and
-    verdict kernels that complete u1*G + u2*Q and decide x(R) == r."""
+    verdict kernels that complete u1*G + u2*Q and decide x(R) == r.
+    qw / beta_per_lookup price the variants (DESIGN.md §4 Roofline, floor):
+    radix-2^qw Q windows, and an (x, y)-only Q table whose lambda lookups
+    form beta * x per addition instead of storing it."""
+    q_table = 1 << (qw - 1)
+    q_windows = (130 + qw - 1) // qw
+    doublings = qw * (q_windows - 1)
+    beta_t = 0 if beta_per_lookup else 1             # beta * x per table entry, or per lambda addition
     table = (GEJ_DOUBLE                      # 2Q
              + FE_SQR + 3 * FE_MUL           # Q' = (x Z^2, y Z^3)
-             + (Q_TABLE - 2) * GEJ_ADD_GE    # 3Q .. Q_TABLE*Q
+             + (q_table - 2) * GEJ_ADD_GE    # 3Q .. q_table*Q
              + FE_MUL                        # Zg
-             + FE_MUL                        # beta * x of the last entry
-             + (Q_TABLE - 2) * (5 * FE_MUL + FE_SQR)   # rescale entries 2..Q_TABLE-1 (+ rho step, beta)
-             + (4 * FE_MUL + FE_SQR))        # rescale entry 1
+             + beta_t * FE_MUL               # beta * x of the last entry
+             + (q_table - 2) * ((4 + beta_t) * FE_MUL + FE_SQR)   # rescale entries 2..q_table-1 (+ rho step, beta)
+             + ((3 + beta_t) * FE_MUL + FE_SQR))                 # rescale entry 1
     if not YFREE:
-        ladder = DOUBLINGS * GEJ_DOUBLE + 2 * Q_WINDOWS * GEJ_ADD_GE + 2 * G_WINDOWS * GEJ_ADD_ZINV
+        ladder = doublings * GEJ_DOUBLE + 2 * q_windows * GEJ_ADD_GE + 2 * G_WINDOWS * GEJ_ADD_ZINV
         compare = 3 * FE_MUL + FE_SQR
         return table + ladder + compare
     to_ew = FE_MUL + FE_SQR                              # Q' = (x w, w^2) on E_w
-    ladder = DOUBLINGS * GEJ_DOUBLE + 2 * Q_WINDOWS * GEJ_ADD_GE + FE_MUL   # + Z = acc.z * Zg
+    ladder = (doublings * GEJ_DOUBLE + 2 * q_windows * GEJ_ADD_GE + FE_MUL   # + Z = acc.z * Zg
+              + (1 - beta_t) * q_windows * FE_MUL)       # beta * x per lambda addition
     g_sum = (2 * G_WINDOWS - 1) * GEJ_ADD_GE             # per-window tables, no doublings
     combine = 16 * FE_MUL + 6 * FE_SQR                   # num, num_{r+n}, den (hkv_finish_kernel)
     inv_chain = 255 * FE_SQR + 15 * FE_MUL               # fe_inv, one per BATCH_INV signatures
