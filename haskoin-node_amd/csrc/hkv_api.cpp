@@ -188,9 +188,10 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
     HKV_TRY(hipEventRecord(e[0], st), "hipEventRecord");
   }
   // A batch of at most half a wave per SIMD (an eighth of the resident grid)
-  // runs the split ecmult (hkv_ecmult_kernel<true>: two lanes per signature
-  // and the G / square-root waves beside them, no separate prologue): a
-  // shorter dependency chain where latency, not issue, bounds the launch.
+  // runs the small-batch kernel (hkv_pair_split_kernel: k1 and k2 chains on
+  // their own waves, two lanes per chain, the signature and square-root waves
+  // beside them, no separate prologue): a shorter dependency chain where
+  // latency, not issue, bounds the launch.
   // Above that the duplicated doublings cost more than the chain saves
   // (measured: a 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms
   // unsplit; the bound itself re-measured in profiles/r02_split_threshold.log).
@@ -204,7 +205,7 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
   // instance, every block resident at its 2-wave allocation
   const bool mid = !split && n_pad <= (size_t)d.grid_max * hkv::WG / 2;
-  const uint32_t blocks = split ? (uint32_t)(n_pad / hkv::SPLIT_SIGS)
+  const uint32_t blocks = split ? 0u  // (the small-batch launch sizes its own grid)
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, mid ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);

@@ -7,20 +7,20 @@
 //      w = x^3 + 7 instead of the sqrt), high-S policy, m = msg mod n, s^-1
 //      (batched), u1 = m/s, u2 = r/s, GLV split of u2, Booth digits. Writes a
 //      SoA intermediate.
-//   2. hkv_ecmult_kernel<SPLIT, ILP> — per-lane table of 1..2^(QW-1) * Q' (8
+//   2. hkv_ecmult_kernel<ILP> — per-lane table of 1..2^(QW-1) * Q' (8
 //      entries at the default radix 16) on an isomorphic curve of E_w (one
 //      common Z, so all Q additions are mixed), then a shared doubling chain
-//      of 132 bits with radix-16 Booth digits for k1*Q' and k2*(lambda Q').
-//      Full-grid launches (SPLIT = false; ILP = the paired-form instance for
-//      mid-size batches) leave B' = u2*Q' to
+//      of 132 bits with radix-16 Booth digits for k1*Q' and k2*(lambda Q')
+//      (ILP = the paired-form instance for mid-size batches); it leaves
+//      B' = u2*Q' to
 //   2b. hkv_finish_kernel, hkv_rare_kernel, hkv_yverdict_kernel — u1*G from
 //      per-window tables, y0 = num/den from "x(u1 G + u2 Q) == r", and the
 //      verdict "y_c^2 == w with the key's parity" (rare lanes: exact sqrt path).
-//      Split launches (small batches, SPLIT = true): waves 4-5 of each
-//      workgroup parse the signature beside the Q tables, then compute u1*G
-//      and the key's sqrt beside the two Q chains (waves 0-1: k1, 2-3: k2),
-//      and half 0 joins exactly (R = A + B, Jacobian x compare); verdicts
-//      leave as a ballot bitmap.
+//   2c. hkv_pair_split_kernel<STD> — small batches (a block) in one launch:
+//      per workgroup 32 signatures on 4 waves (k1 chains, k2 chains, two lanes
+//      per signature; the signature wave: parse, u1*G; the key's sqrt), the
+//      halves joined exactly (R = A + B, Jacobian x compare); STD = standard
+//      inputs (verifyStdInput's parse and hashes inside the same launch).
 //   3. hkv_gtable_kernel    — once per context: the fixed-base tables.
 //   4. hkv_gen_*            — synthetic valid batches (keyless construction,
 //      SURVEY.md §8(c)) for the benchmark and the tests.
@@ -421,20 +421,6 @@ HKV_DEV void sig_lane_g(sc m, const sc& sinv, bool use, uint32_t* __restrict__ i
   for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
   write_gdigits(im, n_pad, i, SL, SH);
 }
-// Both halves from a verify record (waves 4-5 of a split workgroup).
-HKV_DEV void sig_lane(const uint32_t* __restrict__ recs, uint32_t n, uint32_t n_pad, uint32_t mode,
-                      uint32_t* __restrict__ im, uint32_t i, bool& ok, bool& glv_ok, bool& n1, bool& n2) {
-  uint32_t w[24];
-#pragma unroll
-  for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
-  sc r, s, m, sinv;
-  rec_be256(r.v, w, 32);
-  rec_be256(s.v, w, 64);
-  rec_be256(m.v, w, 0);
-  ok = i < n;
-  sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
-  sig_lane_g(m, sinv, ok && glv_ok, im, n_pad, i);
-}
 // flags as the full-grid kernels leave them (hkv_glv_kernel)
 HKV_DEV uint32_t split_flags(bool ok, uint32_t pk_ok, bool glv_ok, bool n1, bool n2) {
   uint32_t f = (ok && (pk_ok & 1u)) ? FLAG_VALID : 0u;
@@ -466,44 +452,6 @@ HKV_DEV void qtab_load(const uint32_t* __restrict__ qs, uint32_t n_lanes, uint32
   a.v[4] = v1.x; a.v[5] = v1.y; a.v[6] = v1.z; a.v[7] = v1.w;
 }
 
-// SPLIT mode keeps each lane's half of the Q table in LDS: entry j holds
-// (x, y) for k1 * Q (half 0) or (beta*x, y) for k2 * lambda(Q) (half 1), as
-// four uint4 quads at [j][quad][thread] (a wave's 64 lanes read 1 KB
-// contiguous per quad). 8 entries x 64 B x 256 threads = 128 KB; with
-// < 1 wave per SIMD the LDS latency replaces an L2 round trip per lookup.
-// (A 16-entry radix-32 table, HKV_QW = 5, does not fit: it stays in scratch
-// as the full-grid kernel's does.)
-// SPLIT launches run < 1 wave per SIMD, so they take the whole register
-// file (196 VGPRs, no spill) instead of the full grid's 4-wave budget.
-#ifndef HKV_SPLIT_WAVES
-#define HKV_SPLIT_WAVES 1
-#endif
-constexpr int QLDS_ENTRIES = QTAB_ENTRIES <= 8 ? QTAB_ENTRIES : 0;
-HKV_DEV void qlds_store(uint4* t, int entry, const fe& x, const fe& y) {
-  uint4* p = t + (size_t)entry * 4 * WG + threadIdx.x;
-  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-  p[WG] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-  p[2 * WG] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
-  p[3 * WG] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
-}
-HKV_DEV void qlds_load(const uint4* t, int entry, fe& x, fe& y) {
-  const uint4* p = t + (size_t)entry * 4 * WG + threadIdx.x;
-  const uint4 v0 = p[0], v1 = p[WG], v2 = p[2 * WG], v3 = p[3 * WG];
-  x.v[0] = v0.x; x.v[1] = v0.y; x.v[2] = v0.z; x.v[3] = v0.w;
-  x.v[4] = v1.x; x.v[5] = v1.y; x.v[6] = v1.z; x.v[7] = v1.w;
-  y.v[0] = v2.x; y.v[1] = v2.y; y.v[2] = v2.z; y.v[3] = v2.w;
-  y.v[4] = v3.x; y.v[5] = v3.y; y.v[6] = v3.z; y.v[7] = v3.w;
-}
-
-// SPLIT (small batches, when one lane per signature would leave the GPU
-// half empty): a workgroup takes 128 signatures; waves 0-1 run k1*Q', waves
-// 2-3 k2*(lambda Q'), each with its own doubling chain (the slot loops become
-// wave-uniform, so each wave issues half the additions), and the halves meet
-// in LDS for one Jacobian addition. The per-signature dependency chain
-// shrinks by about a quarter; total work grows by the duplicated doublings
-// and table, so large batches use SPLIT = false. SPLIT launches use the
-// paired-product group forms; the full grid keeps the plain forms (its 4
-// waves per SIMD already fill the issue slots) except for mid-size batches.
 template <bool ILP>
 HKV_DEV void ec_double(gej& acc) {
   if constexpr (ILP) gej_double_ilp(acc, acc);
@@ -519,52 +467,16 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
                        bool valid, gej& A, bool& ainf);
 HKV_DEV void gej_add_var(gej& acc, bool& inf, const gej& b, bool binf);
 HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]);
-// waves 4-5 of the split kernel: A = u1 G and the key's y0 = sqrt(w) of its
-// parity into aux for half 0's join
-HKV_DEV void split_aux_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab,
-                            uint32_t* __restrict__ aux, uint32_t i, bool valid, uint32_t flags, const fe& w) {
-  gej A;
-  bool ainf;
-  gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
-  fe y0, y2, ny;
-  fe_sqrt_cand(y0, w);
-  fe_sqr(y2, y0);
-  const bool is_sq = fe_equal(y2, w);
-  fe_normalize(y0);
-  fe_neg(ny, y0);
-  fe_normalize(ny);
-  if ((y0.v[0] & 1u) != ((flags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
-    aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
-    aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
-    aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
-  }
-  aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | (is_sq ? AUXF_SQ : 0u);
-  __threadfence_block();
-}
-// ILP: the paired-product group forms. The split kernel uses them (< 1 wave
-// per SIMD); full-grid launches of mid-size batches (at most 2 waves per
-// SIMD: 32k-131k signatures) take the <false, true> instance, which is
-// allocated for 2 waves per SIMD (no spill).
-template <bool SPLIT, bool ILP>
-__global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVES : (ILP ? 2 : HKV_ECMULT_WAVES)) hkv_ecmult_kernel(uint32_t* __restrict__ im, uint32_t n,
-                                                        uint32_t n_pad, const uint32_t* __restrict__ gtab,
-                                                        uint32_t* __restrict__ qs,
-                                                        uint32_t* __restrict__ bits, uint32_t n_words,
-                                                        unsigned long long* __restrict__ clk,
-                                                        uint32_t* __restrict__ aux,
-                                                        const uint32_t* __restrict__ recs, uint32_t mode) {
-  // SPLIT: half 1 hands (X, Y, Z, inf) to half 0 through LDS, word-major [25][SPLIT_SIGS]
-  __shared__ uint32_t xch[SPLIT ? 25 * SPLIT_SIGS : 1];
-  constexpr bool QLDS = SPLIT && QLDS_ENTRIES > 0;
-  __shared__ __attribute__((aligned(16))) uint4 qlds[QLDS ? QLDS_ENTRIES * 4 * WG : 1];
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr uint32_t PER_WG = SPLIT ? SPLIT_SIGS : WG;
-  const int half = SPLIT ? wv / (SPLIT_SIGS / 64) : 0;  // wave-uniform
-  const uint32_t sub = SPLIT ? (threadIdx.x & (PER_WG - 1)) : threadIdx.x;
-
+// ILP: the paired-product group forms; full-grid launches of mid-size
+// batches (at most 2 waves per SIMD: 32k-131k signatures) take the <true>
+// instance, which is allocated for 2 waves per SIMD (no spill). The 1M
+// launch keeps the plain forms: its 4 waves per SIMD already fill the issue
+// slots.
+template <bool ILP>
+__global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_kernel(uint32_t* __restrict__ im,
+                                                                                 uint32_t n, uint32_t n_pad,
+                                                                                 uint32_t* __restrict__ qs,
+                                                                                 unsigned long long* __restrict__ clk) {
   const uint32_t n_lanes = gridDim.x * WG;
   const uint32_t lane = blockIdx.x * WG + threadIdx.x;
   // optional clock probe (hkv_profile_clock): shader-clock and constant-rate
@@ -575,53 +487,12 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
     clk[1] = wall_clock64();
   }
 
-  for (uint32_t base = blockIdx.x * PER_WG; base < n_pad; base += gridDim.x * PER_WG) {
-    const uint32_t i = base + sub;
-    uint32_t flags;
-    bool valid;
+  for (uint32_t base = blockIdx.x * WG; base < n_pad; base += gridDim.x * WG) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+    const bool valid = (i < n) && (flags & FLAG_VALID);
     ge q;
-    if (SPLIT) {
-      // waves 4-5 parse the signature (s^-1, u1, u2, GLV, digits) while
-      // waves 0-3 parse the key and build their tables; barrier P publishes
-      // the digits, r and flags; then waves 4-5 compute A = u1 G and the
-      // key's y0 = sqrt(w) for half 0's join, taking part in the join's
-      // two barriers and nothing else
-      if (half == 2) {
-        bool ok, glv_ok, n1, n2;
-        sig_lane(recs, n, n_pad, mode, im, i, ok, glv_ok, n1, n2);
-        uint32_t kw[REC_WORDS];
-#pragma unroll
-        for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
-        fe x, w;
-        uint32_t pflags = 0;
-        const bool pk = pubkey_parse_rec_w(kw, x, w, pflags) && i < n;
-        flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
-        im[(size_t)IM_FLAGS * n_pad + i] = flags;
-        __threadfence_block();
-        __syncthreads();  // barrier P
-        split_aux_lane(im, n_pad, gtab, aux, i, (flags & FLAG_VALID) != 0, flags, w);
-        __syncthreads();  // barrier A: aux and half 1's sum are published
-        __syncthreads();  // barrier B: half 0 has read them
-        continue;
-      }
-      uint32_t kw[REC_WORDS];
-#pragma unroll
-      for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
-      fe w;
-      uint32_t pflags;
-      const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
-      fe xw, ww;  // Q' = (x w, w^2) on E_w
-      fe_mul(xw, q.x, w);
-      fe_sqr(ww, w);
-      q.x = xw;
-      q.y = ww;
-      if (!pk) ge_set_g(q);  // dummy point (the lane is invalid: its digits are zero)
-      __syncthreads();  // barrier P: the signature waves' digits, r and flags are in im
-      flags = im[(size_t)IM_FLAGS * n_pad + i];
-      valid = (i < n) && (flags & FLAG_VALID);
-    } else {
-      flags = im[(size_t)IM_FLAGS * n_pad + i];
-      valid = (i < n) && (flags & FLAG_VALID);
+    {
       fe x, w;  // IM_QY holds w = x^3 + 7: Q' = (x w, w^2) on E_w
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -637,8 +508,7 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
     // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
     // Pass 1 streams raw entries to the lane's scratch (z-ratios H_j parked in
     // the beta*x slot of entry j-1); pass 2 walks back rescaling every entry
-    // to the common Z (rho_j = prod_{k>j} H_k) and writes beta*x (SPLIT mode:
-    // the rescaled entries of the wave's half go to LDS instead).
+    // to the common Z (rho_j = prod_{k>j} H_k) and writes beta*x.
     fe Zg;
     {
       gej p2, pj;
@@ -673,7 +543,6 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
         fe bx;
         fe_mul(bx, pj.x, beta);
         qtab_store(qs, n_lanes, lane, QTAB_ENTRIES - 1, 4, bx);
-        if (QLDS) qlds_store(qlds, QTAB_ENTRIES - 1, half ? bx : pj.x, pj.y);
       }
       fe rho;
       fe_set_u32(rho, 1);
@@ -690,11 +559,6 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
         fe_mul(x, x, t);
         fe_mul(t, t, rho);
         fe_mul(y, y, t);
-        if (QLDS) {
-          if (half) fe_mul(x, x, beta);
-          qlds_store(qlds, j, x, y);
-          continue;
-        }
         qtab_store(qs, n_lanes, lane, j, 0, x);
         qtab_store(qs, n_lanes, lane, j, 2, y);
         fe_mul(x, x, beta);
@@ -725,17 +589,12 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
       // Q terms: slot 0 = k1 * Q', slot 1 = k2 * lambda(Q')
 #pragma unroll 1
       for (int slot = 0; slot < 2; ++slot) {
-        if (SPLIT && slot != half) continue;
         const int dg = slot == 0 ? d1 : d2;
         const bool take = dg != 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
         fe tx, ty;
-        if (QLDS) {
-          qlds_load(qlds, (slot == 0 ? i1 : i2), tx, ty);
-        } else {
-          qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
-          qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
-        }
+        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
+        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
         fe_cneg(ty, ty, neg);
         const bool was_inf = inf;
         ec_accumulate<ILP>(acc, inf, acc.z, tx, ty, take);
@@ -746,75 +605,16 @@ __global__ void __launch_bounds__(SPLIT ? SPLIT_TPB : WG, SPLIT ? HKV_SPLIT_WAVE
       dw = dw_next;
     }
 
-    if (!SPLIT) {  // hand B' = (X, Y, Z acc * Zg) on E_w to the finish kernel
-      fe zt;
-      fe_mul(zt, acc.z, Zg);
+    // hand B' = (X, Y, Z acc * Zg) on E_w to the finish kernel
+    fe zt;
+    fe_mul(zt, acc.z, Zg);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
-        im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
-        im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
-      }
-      im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
-      continue;
+    for (int k = 0; k < 8; ++k) {
+      im[(size_t)(IM_BX + k) * n_pad + i] = acc.x.v[k];
+      im[(size_t)(IM_BX + 8 + k) * n_pad + i] = acc.y.v[k];
+      im[(size_t)(IM_BX + 16 + k) * n_pad + i] = zt.v[k];
     }
-
-    // ---- SPLIT: the halves meet; B = phi^-1(B') = (X, Y, Z acc Zg y0) on E,
-    // R = A + B exactly, x compare ----
-    if (half == 1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        xch[k * PER_WG + sub] = acc.x.v[k];
-        xch[(8 + k) * PER_WG + sub] = acc.y.v[k];
-        xch[(16 + k) * PER_WG + sub] = acc.z.v[k];
-      }
-      xch[24 * PER_WG + sub] = inf ? 1u : 0u;
-    }
-    __syncthreads();  // barrier A
-    bool accept = false;
-    if (half == 0) {
-      gej b;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        b.x.v[k] = xch[k * PER_WG + sub];
-        b.y.v[k] = xch[(8 + k) * PER_WG + sub];
-        b.z.v[k] = xch[(16 + k) * PER_WG + sub];
-      }
-      const bool binf = xch[24 * PER_WG + sub] != 0;
-      // acc + b, both Jacobian on the same isomorphic curve: rescale acc by
-      // b.z (same point), then b enters as (X2, Y2) against scale Z1
-      gej_add_var(acc, inf, b, binf);
-      gej A;
-      fe y0;
-      uint32_t r[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
-        A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
-        A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
-        y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
-        r[k] = im[(size_t)(IM_R + k) * n_pad + i];
-      }
-      const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
-      gej bb;
-      bb.x = acc.x;
-      bb.y = acc.y;
-      fe zt;
-      fe_mul(zt, acc.z, Zg);
-      fe_mul(bb.z, zt, y0);
-      bool rinf = (af & AUXF_AINF) != 0;
-      gej_add_var(A, rinf, bb, inf);
-      accept = valid && (af & AUXF_SQ) && !rinf && x_matches_r(A.x, A.z, r);
-    }
-    __syncthreads();  // barrier B: the next signature group's writers of xch / aux wait for the readers
-    const uint64_t ball = __ballot(accept);
-    if ((threadIdx.x & 63) == 0 && half == 0) {
-      // n_words bounds the caller's bitmap ((n + 31) / 32 words when the
-      // verdicts go straight to the API's output, n_pad / 32 for d.bits)
-      const uint32_t wi = (base + (sub & ~63u)) / 32;
-      if (wi < n_words) bits[wi] = (uint32_t)ball;
-      if (wi + 1 < n_words) bits[wi + 1] = (uint32_t)(ball >> 32);
-    }
+    im[(size_t)IM_FLAGS * n_pad + i] = flags | (inf ? FLAG_BINF : 0u);
   }
   if (clk != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
     clk[2] = clock64();
@@ -1959,22 +1759,20 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
-// split: small batches (SPLIT_SIGS signatures per workgroup, no separate
-// prologue); mid: full-grid batches of at most 2 waves per SIMD, the
-// paired-form instance at a 2-wave register allocation
+// split: small batches (hkv_pair_split_kernel, PAIR_SIGS signatures per
+// workgroup, no separate prologue); mid: full-grid batches of at most 2 waves
+// per SIMD, the paired-form instance at a 2-wave register allocation
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool mid,
                          unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st) {
-  const uint32_t* rw = (const uint32_t*)recs;
   if (split)
     hipLaunchKernelGGL(hkv_pair_split_kernel<false>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, aux, const_cast<uint32_t*>(rw), mode, clk, StdArgs{});
+                       gtab, qs, bits, n_words, aux, const_cast<uint32_t*>((const uint32_t*)recs), mode, clk,
+                       StdArgs{});
   else if (mid)
-    hipLaunchKernelGGL((hkv_ecmult_kernel<false, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, aux, rw, mode);
+    hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
   else
-    hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, gtab, qs, bits,
-                       n_words, clk, aux, rw, mode);
+    hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
   return hipGetLastError();
 }
 // small batches of standard inputs: parse, the Q chains, the script checks,
@@ -2046,7 +1844,7 @@ hipError_t launch_gen_sign(uint64_t seed, uint32_t n, const uint8_t* priv, const
   return hipGetLastError();
 }
 hipError_t ecmult_max_blocks_per_cu(int* out) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel<false, false>, WG, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, hkv_ecmult_kernel<false>, WG, 0);
 }
 
 }  // namespace hkv

@@ -70,21 +70,10 @@ constexpr uint32_t FLAG_VALID = 1u, FLAG_NEG1 = 2u, FLAG_NEG2 = 4u, FLAG_GLV_OVF
 // leaves B' = (X, Y, Z) over the Q-digit words; the finish kernel adds the
 // u1 * G sum from per-window tables and reduces "x(u1 G + u2 Q) == r" to
 // y_c = num / den, accepted iff y_c^2 == w with the key's y parity. Small
-// batches (the split ecmult) run the u1 * G sum and the key's square root as
-// waves 4-5 of each workgroup, beside the two Q chains, and join exactly in
-// the kernel (configs[0] block 755 -> 703 us, configs[2] 796 -> 744 us;
-// profiles/r02_variants_split_yfree.log); waves 4-5 also parse the
-// signatures while waves 0-3 build the Q tables (configs[0] 701 -> 696 us,
-// profiles/r02_variants_split_fuse.log).
-// HKV_SPLIT_SIGS: signatures per split workgroup (128: waves 0-1 / 2-3 / 4-5
-// are the halves and the G-sum waves; 64: one wave each, 192 threads)
-#ifndef HKV_SPLIT_SIGS
-#define HKV_SPLIT_SIGS 128
-#endif
-static_assert(HKV_SPLIT_SIGS == 64 || HKV_SPLIT_SIGS == 128, "split workgroups take 64 or 128 signatures");
-constexpr int SPLIT_SIGS = HKV_SPLIT_SIGS;
-constexpr int SPLIT_TPB = 3 * SPLIT_SIGS;
-// waves 4-5's output for the join (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
+// batches (hkv_pair_split_kernel, §2c) run the u1 * G sum and the key's
+// square root on their own waves beside the two Q chains and join exactly in
+// the kernel.
+// the small-batch kernel's signature / square-root waves' output for the join (SoA, its own buffer): A = u1 G (24 words), y0 (8), flags
 enum : int { AUX_AX = 0, AUX_Y0 = 24, AUX_FLAGS = 32, AUX_SQ = 33, AUX_WORDS = 34 };  // AUX_SQ: the pair kernel's sqrt wave
 constexpr uint32_t AUXF_AINF = 1u, AUXF_SQ = 2u;
 constexpr uint32_t FLAG_YODD = 16u;      // the key's y is odd (prefix 03/07, or the 04 key's y)

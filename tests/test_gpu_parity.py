@@ -388,10 +388,11 @@ def test_config5_ibd_16m_sharded_bitmap(torch, ver, coracle):
 
 
 def test_split_lane_ecmult_matches_full_grid(torch, ver, coracle):
-    """Small batches run two lanes per signature (hkv_ecmult_kernel<true>,
-    chosen when the padded batch fills at most an eighth of the resident
-    grid, 32,768 signatures on an MI355X);
-    large ones one lane (<false>). The same adversarial records verified in
+    """Small batches run the small-batch kernel (hkv_pair_split_kernel<false>:
+    k1 and k2 chains on their own waves, two lanes per chain; chosen when the
+    padded batch fills at most an eighth of the resident grid, 32,768
+    signatures on an MI355X); large ones one lane per signature
+    (hkv_ecmult_kernel + the finish kernels). The same adversarial records verified in
     both launch shapes give identical verdicts, equal to the C oracle on a
     slice, in both modes."""
     from hkv import adversarial

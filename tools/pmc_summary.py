@@ -21,13 +21,20 @@ from collections import defaultdict
 
 
 def kname(raw: str) -> str:
-    """hkv::hkv_ecmult_kernel<false, false>(...) -> hkv_ecmult_kernel; <false, true> -> _mid; <true, ...> -> _split."""
+    """Kernel name without the namespace / argument list. The ecmult instances:
+    round 3 hkv_ecmult_kernel<ILP> (<false> full grid, <true> -> _mid) and
+    hkv_pair_split_kernel<STD> (<false> -> _rec, <true> -> _std); the round-2
+    hkv_ecmult_kernel<SPLIT, ILP> names map as before (<false, false> full
+    grid, <false, true> _mid, <true, *> _split)."""
     k = raw.split("(")[0].replace("hkv::", "")
     if k.startswith("void "):
         k = k[5:]
-    # hkv_ecmult_kernel<SPLIT, ILP>: <false, false> full grid, <false, true> mid-size, <true, *> split
     k = k.replace("<false, false>", "").replace("<false, true>", "_mid")
     k = k.replace("<true, true>", "_split").replace("<true, false>", "_split")
+    if k.startswith("hkv_pair_split_kernel"):
+        return k.replace("<false>", "_rec").replace("<true>", "_std")
+    if k.startswith("hkv_ecmult_kernel"):
+        return k.replace("<false>", "").replace("<true>", "_mid")
     return k.replace("<false>", "").replace("<true>", "_split")
 
 
