@@ -210,7 +210,7 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
   HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, mid,
-                             d.profile ? d.clk : nullptr, d.aux, d_records, mode, st),
+                             d.profile ? d.clk : nullptr, d.aux, d_records, mode, (uint32_t)d.n_cu, st),
           "ecmult launch");
   // full-grid batches: the finish kernels add u1 * G and decide x(R) == r
   // through y_c = num / den (hkv_kernels.hip §2b). The rare-lane count is
@@ -443,7 +443,8 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
   }
   HKV_TRY(hkv::launch_std_verify_split(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
                                        (uint32_t)n_pad, forkid, static_cast<uint8_t*>(recs), d.im, d.gtab, d.qs,
-                                       d.aux, out_bits, (uint32_t)((n + 31) / 32), d.profile ? d.clk : nullptr, st),
+                                       d.aux, out_bits, (uint32_t)((n + 31) / 32), d.profile ? d.clk : nullptr,
+                                       (uint32_t)d.n_cu, st),
           "std-input verify launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");

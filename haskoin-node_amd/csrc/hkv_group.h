@@ -226,6 +226,10 @@ HKV_DEV void fe_bc1(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = dpp_bc1(a.v[i]);
 }
+HKV_DEV void fe_bc0(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = dpp_bc0(a.v[i]);
+}
 // r = a on the even lane, b on the odd lane (odd: all ones on odd lanes)
 HKV_DEV void fe_sel(fe& r, const fe& a, const fe& b, uint32_t odd) {
 #pragma unroll

@@ -29,13 +29,14 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
                            hipStream_t st);
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool mid,
-                         unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st);
+                         unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, uint32_t n_cu,
+                         hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
-                                   hipStream_t st);
+                                   uint32_t n_cu, hipStream_t st);
 // y-free full-grid batches: u1 * G, the y0 = num / den reduction and the verdict bitmap
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st);

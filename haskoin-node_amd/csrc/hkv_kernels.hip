@@ -691,6 +691,283 @@ struct StdArgs {
   int32_t forkid;
 };
 
+// Pair-form pieces shared by the small-batch kernels (2c, 2d). Each chain
+// lane keeps its own coordinate of every table entry in LDS: ql is one chain
+// wave's [QTAB_ENTRIES][8][64] table (x, or beta * x when half = 1, on the
+// even lane; y on the odd lane).
+typedef uint32_t QLane[QTAB_ENTRIES][8][64];
+
+// j * q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg (q affine
+// on its own curve; the a = 0 formulas never use b). Both lanes of a pair
+// build it; entries stream through the lane's qs scratch, then the backward
+// rescale writes the LDS table. Returns Zg.
+HKV_DEV void pair_table(const ge& q, int half, uint32_t odd, uint32_t* __restrict__ qs, uint32_t n_lanes,
+                        uint32_t qlane, QLane& ql, uint32_t ln, fe& Zg) {
+  gej p2, pj;
+  gej_set_ge(p2, q);
+  gej_double(p2, p2);  // 2Q (Jacobian, scale Z2)
+  fe z2, qx, qy;       // Q' = phi_Z2(Q) = (x Z2^2, y Z2^3)
+  fe_sqr(z2, p2.z);
+  fe_mul(qx, q.x, z2);
+  fe_mul(z2, z2, p2.z);
+  fe_mul(qy, q.y, z2);
+  qtab_store(qs, n_lanes, qlane, 0, 0, qx);
+  qtab_store(qs, n_lanes, qlane, 0, 2, qy);
+  qtab_store(qs, n_lanes, qlane, 1, 0, p2.x);
+  qtab_store(qs, n_lanes, qlane, 1, 2, p2.y);
+  pj.x = p2.x;
+  pj.y = p2.y;
+  fe_set_u32(pj.z, 1);
+#pragma unroll 1
+  for (int j = 2; j < QTAB_ENTRIES; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
+    bool hz, rz;
+    fe h;
+    gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
+    qtab_store(qs, n_lanes, qlane, j, 0, pj.x);
+    qtab_store(qs, n_lanes, qlane, j, 2, pj.y);
+    qtab_store(qs, n_lanes, qlane, (j - 1), 4, h);
+  }
+  fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
+  fe beta;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) beta.v[k] = FE_BETA[k];
+  auto put = [&](int j, const fe& x, const fe& y) {
+    fe v;
+    fe_sel(v, x, y, odd);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ql[j][k][ln] = v.v[k];
+  };
+  {
+    fe bx = pj.x;
+    if (half) fe_mul(bx, pj.x, beta);
+    put(QTAB_ENTRIES - 1, bx, pj.y);
+  }
+  fe rho;
+  fe_set_u32(rho, 1);
+#pragma unroll 1
+  for (int j = QTAB_ENTRIES - 2; j >= 0; --j) {
+    fe x, y, t;
+    if (j >= 1) {
+      qtab_load(qs, n_lanes, qlane, j, 4, t);  // H_{j+1}
+      fe_mul(rho, rho, t);
+    }
+    qtab_load(qs, n_lanes, qlane, j, 0, x);
+    qtab_load(qs, n_lanes, qlane, j, 2, y);
+    fe_sqr(t, rho);
+    fe_mul(x, x, t);
+    fe_mul(t, t, rho);
+    fe_mul(y, y, t);
+    if (half) fe_mul(x, x, beta);
+    put(j, x, y);
+  }
+}
+
+// The windows w_hi..w_lo (radix 16, top first) of one chain in pair form,
+// from infinity: P = X | Y, Z on the odd lane. half 0 takes k1's digits,
+// half 1 k2's; negh: the GLV half is negative.
+HKV_DEV void pair_chain(fe& P, fe& Z, bool& inf, const QLane& ql, const uint32_t* __restrict__ im, uint32_t n_pad,
+                        uint32_t i, bool valid, bool negh, int half, uint32_t odd, uint32_t ln, int w_hi, int w_lo) {
+  inf = true;
+  fe_set_zero(P);
+  fe_set_zero(Z);
+  uint32_t dw = valid ? im[(size_t)(IM_DIG + w_hi) * n_pad + i] : DIG_ZERO;
+#pragma unroll 1
+  for (int win = w_hi; win >= w_lo; --win) {
+    const int dg = half ? (int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS : (int)(dw & QDIG_MASK) - QBIAS;
+    const int mg = dg < 0 ? -dg : dg;
+    const int ie = mg ? mg - 1 : 0;
+    const uint32_t dw_next = (win > w_lo && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
+    if (win != w_hi) {
+#pragma unroll 1
+      for (int d = 0; d < QW; ++d) {
+        if (!inf) pair_double(P, Z, odd);
+      }
+    }
+    const bool take = dg != 0;
+    const bool neg = (dg < 0) != negh;
+    fe T;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) T.v[k] = ql[ie][k][ln];
+    fe_cneg(T, T, neg && odd);  // y -> -y on the odd lane
+    const bool was_inf = inf;
+    pair_accumulate(P, Z, inf, T, take, odd);
+    if (__any(take && was_inf)) pair_accumulate_from_inf(P, Z, inf, T, take && was_inf);
+    dw = dw_next;
+  }
+}
+
+// a pair-form chain's sum (X | Y, Z on the odd lane) to LDS: word-major
+// [25][sigs] (X, Y, Z, inf), signature slot c
+HKV_DEV void pair_publish(uint32_t* __restrict__ xch, int sigs, uint32_t c, const fe& P, const fe& Z, bool inf,
+                          uint32_t odd) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (!odd) xch[k * sigs + c] = P.v[k];
+    else {
+      xch[(8 + k) * sigs + c] = P.v[k];
+      xch[(16 + k) * sigs + c] = Z.v[k];
+    }
+  }
+  if (odd) xch[24 * sigs + c] = inf ? 1u : 0u;
+}
+HKV_DEV void xch_read(const uint32_t* __restrict__ xch, int sigs, uint32_t c, gej& b, bool& binf) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    b.x.v[k] = xch[k * sigs + c];
+    b.y.v[k] = xch[(8 + k) * sigs + c];
+    b.z.v[k] = xch[(16 + k) * sigs + c];
+  }
+  binf = xch[24 * sigs + c] != 0;
+}
+HKV_DEV void xch_write(uint32_t* __restrict__ xch, int sigs, uint32_t c, const gej& b, bool binf) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    xch[k * sigs + c] = b.x.v[k];
+    xch[(8 + k) * sigs + c] = b.y.v[k];
+    xch[(16 + k) * sigs + c] = b.z.v[k];
+  }
+  xch[24 * sigs + c] = binf ? 1u : 0u;
+}
+
+// ---- the roles both small-batch kernels share ----
+// the key words of signature i (record words 24..41; STD: parsed from its
+// input, which x receives)
+template <bool STD>
+HKV_DEV void key_words_of(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs, const StdArgs& sa,
+                          uint32_t kw[REC_WORDS], StdIn& x) {
+  if constexpr (STD) {
+    std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid);
+    std_key_words(kw, x);
+  } else {
+#pragma unroll
+    for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
+  }
+}
+// Q' = (x w, w^2) on E_w of signature i's key (G, a dummy, for a key that
+// does not parse: the lane's digits are zero)
+template <bool STD>
+HKV_DEV void key_point(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs, const StdArgs& sa, ge& q) {
+  uint32_t kw[REC_WORDS];
+  StdIn xs = {};
+  key_words_of<STD>(i, n, recs, sa, kw, xs);
+  fe w;
+  uint32_t pflags;
+  const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
+  fe xw, ww;
+  fe_mul(xw, q.x, w);
+  fe_sqr(ww, w);
+  q.x = xw;
+  q.y = ww;
+  if (!pk) ge_set_g(q);
+}
+// The signature wave, first half (lanes with on): range and high-S policy,
+// s^-1, u2, the GLV split and Booth digits, r and the flags into im.
+template <bool STD>
+HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* __restrict__ im,
+                            const uint32_t* __restrict__ recs, const StdArgs& sa, StdIn& x, sc& m, sc& sinv,
+                            bool& use, uint32_t& flags) {
+  flags = 0;
+  use = false;
+  if (!on) return;
+  bool ok = i < n, glv_ok, n1, n2;
+  uint32_t kw[REC_WORDS];
+  key_words_of<STD>(i, n, recs, sa, kw, x);
+  sc r, s;
+  if constexpr (STD) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { r.v[k] = x.r[k]; s.v[k] = x.s[k]; }
+    ok = ok && x.ok;
+  } else {
+    uint32_t w[24];
+#pragma unroll
+    for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
+    rec_be256(r.v, w, 32);
+    rec_be256(s.v, w, 64);
+    rec_be256(m.v, w, 0);
+  }
+  sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
+  use = ok && glv_ok;
+  fe kx, kwv;
+  uint32_t pflags = 0;
+  const bool pk = pubkey_parse_rec_w(kw, kx, kwv, pflags) && i < n;
+  flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
+  im[(size_t)IM_FLAGS * n_pad + i] = flags;
+}
+// The signature wave, second half (whole wave: the STD hashes are
+// block-synchronous): STD — the script checks, the sighash and the input's
+// verify record; then u1 = m / s and A = u1 G into aux.
+template <bool STD>
+HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im,
+                           const uint32_t* __restrict__ gtab, uint32_t* __restrict__ aux, uint32_t* __restrict__ recs,
+                           const StdArgs& sa, uint32_t* shabuf, StdIn& x, sc m, const sc& sinv, bool use,
+                           uint32_t flags) {
+  uint32_t stdok = 0;
+  if constexpr (STD) {
+    uint32_t* r32 = recs + (size_t)(on && i < n ? i : 0) * REC_WORDS;
+    if (!on) x.ok = false;
+    uint32_t d[8];
+    // (r32 is scratch until the record is written: words 0-7 for a BIP143
+    // SINGLE hashOutputs, 8-31 for the tx's BIP143 hashes, which the fused
+    // launch computes per input instead of an index-kernel pass)
+    const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8);
+    if (on) {
+      if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
+      uint32_t w[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = !x.ok ? 0u : (live ? d[k] : (k == 0 ? 1u : 0u));
+      rec_be256(m.v, w, 0);
+      stdok = x.ok ? AUXF_STDOK : 0u;
+    }
+  }
+  if (!on) return;
+  sig_lane_g(m, sinv, use, im, n_pad, i);
+  gej A;
+  bool ainf;
+  gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
+    aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
+    aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
+  }
+  aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | stdok;
+}
+// The key's y0 = sqrt(w) with the key's y parity, and whether w is a square
+template <bool STD>
+HKV_DEV void sqrt_lane(uint32_t i, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ recs, const StdArgs& sa,
+                       uint32_t* __restrict__ aux) {
+  uint32_t kw[REC_WORDS];
+  StdIn xs = {};
+  key_words_of<STD>(i, n, recs, sa, kw, xs);
+  fe x, w, y0, y2, ny;
+  uint32_t pflags = 0;
+  (void)pubkey_parse_rec_w(kw, x, w, pflags);
+  fe_sqrt_cand(y0, w);
+  fe_sqr(y2, y0);
+  const bool is_sq = fe_equal(y2, w);
+  fe_normalize(y0);
+  fe_neg(ny, y0);
+  fe_normalize(ny);
+  if ((y0.v[0] & 1u) != ((pflags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
+  aux[(size_t)AUX_SQ * n_pad + i] = is_sq ? AUXF_SQ : 0u;
+}
+// A, y0, the join flags and r of signature i (aux / im)
+HKV_DEV void join_inputs(const uint32_t* __restrict__ im, const uint32_t* __restrict__ aux, uint32_t n_pad,
+                         uint32_t i, gej& A, fe& y0, uint32_t r[8], uint32_t& af, bool& is_sq) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
+    A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
+    A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
+    y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+    r[k] = im[(size_t)(IM_R + k) * n_pad + i];
+  }
+  af = aux[(size_t)AUX_FLAGS * n_pad + i];
+  is_sq = aux[(size_t)AUX_SQ * n_pad + i] != 0;
+}
+
 template <bool STD>
 __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                                      uint32_t n_pad,
@@ -704,7 +981,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
                                                                      StdArgs sa) {
   // per chain wave: QTAB_ENTRIES entries x 8 words x 64 lanes (each lane keeps
   // its own coordinate of every entry: x or beta*x on the even lane, y on the odd)
-  __shared__ uint32_t qlds[2][QTAB_ENTRIES][8][64];
+  __shared__ QLane qlds[2];
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t shabuf[STD ? 16 * WG : 1];  // std_hash's per-lane SHA-256 blocks ([word][thread])
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -719,87 +996,22 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
     if (stamp) clk[4 + slot] = wall_clock64();
   };
   if (wv == 0) mark(STAMP_START);
-  // the key words of signature i (record words 24..41; STD: parsed from its
-  // input, which x receives)
-  auto key_words = [&](uint32_t i, uint32_t kw[REC_WORDS], StdIn& x) {
-    if constexpr (STD) {
-      std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid);
-      std_key_words(kw, x);
-    } else {
-#pragma unroll
-      for (int k = 0; k < REC_WORDS; ++k) kw[k] = (k >= 24 && i < n) ? recs[(size_t)i * REC_WORDS + k] : 0u;
-    }
-  };
 
   for (uint32_t base = blockIdx.x * PAIR_SIGS; base < n_pad; base += gridDim.x * PAIR_SIGS) {
     if (wv == 2) {
       // ---- the signature: u2 half (lanes 0-31), then the u1 half and A = u1 G ----
       const uint32_t i = base + ln;
-      uint32_t flags = 0;
-      bool use = false;
+      const bool on = ln < PAIR_SIGS;
+      uint32_t flags;
+      bool use;
       sc sinv, m;
       StdIn x = {};
-      if (ln < PAIR_SIGS) {
-        bool ok = i < n, glv_ok, n1, n2;
-        uint32_t kw[REC_WORDS];
-        key_words(i, kw, x);
-        sc r, s;
-        if constexpr (STD) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { r.v[k] = x.r[k]; s.v[k] = x.s[k]; }
-          ok = ok && x.ok;
-        } else {
-          uint32_t w[24];
-#pragma unroll
-          for (int k = 0; k < 24; ++k) w[k] = i < n ? recs[(size_t)i * REC_WORDS + k] : 0u;
-          rec_be256(r.v, w, 32);
-          rec_be256(s.v, w, 64);
-          rec_be256(m.v, w, 0);
-        }
-        sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
-        use = ok && glv_ok;
-        fe kx, kwv;
-        uint32_t pflags = 0;
-        const bool pk = pubkey_parse_rec_w(kw, kx, kwv, pflags) && i < n;
-        flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
-        im[(size_t)IM_FLAGS * n_pad + i] = flags;
-        __threadfence_block();
-      }
+      sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags);
+      __threadfence_block();
       mark(STAMP_SIG);
       __syncthreads();  // barrier P
-      uint32_t stdok = 0;
-      if constexpr (STD) {
-        // the script checks and the sighash (whole wave: block-synchronous SHA-256)
-        uint32_t* r32 = recs + (size_t)(ln < PAIR_SIGS && i < n ? i : 0) * REC_WORDS;
-        if (ln >= PAIR_SIGS) x.ok = false;
-        uint32_t d[8];
-        // (r32 is scratch until the record is written: words 0-7 for a BIP143
-        // SINGLE hashOutputs, 8-31 for the tx's BIP143 hashes, which the
-        // fused launch computes per input instead of an index-kernel pass)
-        const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8);
-        if (ln < PAIR_SIGS) {
-          if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
-          uint32_t w[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) w[k] = !x.ok ? 0u : (live ? d[k] : (k == 0 ? 1u : 0u));
-          rec_be256(m.v, w, 0);
-          stdok = x.ok ? AUXF_STDOK : 0u;
-        }
-      }
-      if (ln < PAIR_SIGS) {
-        sig_lane_g(m, sinv, use, im, n_pad, i);
-        gej A;
-        bool ainf;
-        gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
-          aux[(size_t)(AUX_AX + 8 + k) * n_pad + i] = A.y.v[k];
-          aux[(size_t)(AUX_AX + 16 + k) * n_pad + i] = A.z.v[k];
-        }
-        aux[(size_t)AUX_FLAGS * n_pad + i] = (ainf ? AUXF_AINF : 0u) | stdok;
-        __threadfence_block();
-      }
+      sig_wave_gsum<STD>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
+      __threadfence_block();
       mark(STAMP_GSUM);
       __syncthreads();  // barrier A
       __syncthreads();  // barrier B
@@ -808,26 +1020,8 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
     if (wv == 3) {
       // ---- the key's y0 = sqrt(w) with the key's y parity (lanes 0-31) ----
       __syncthreads();  // barrier P (nothing to wait for: the key bytes are input)
-      const uint32_t i = base + ln;
-      if (ln < PAIR_SIGS) {
-        uint32_t kw[REC_WORDS];
-        StdIn xs = {};
-        key_words(i, kw, xs);
-        fe x, w, y0, y2, ny;
-        uint32_t pflags = 0;
-        (void)pubkey_parse_rec_w(kw, x, w, pflags);
-        fe_sqrt_cand(y0, w);
-        fe_sqr(y2, y0);
-        const bool is_sq = fe_equal(y2, w);
-        fe_normalize(y0);
-        fe_neg(ny, y0);
-        fe_normalize(ny);
-        if ((y0.v[0] & 1u) != ((pflags & FLAG_YODD) ? 1u : 0u)) y0 = ny;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) aux[(size_t)(AUX_Y0 + k) * n_pad + i] = y0.v[k];
-        aux[(size_t)AUX_SQ * n_pad + i] = is_sq ? AUXF_SQ : 0u;
-        __threadfence_block();
-      }
+      if (ln < PAIR_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
+      __threadfence_block();
       mark(STAMP_SQRT);
       __syncthreads();  // barrier A
       __syncthreads();  // barrier B
@@ -838,85 +1032,11 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
     const int half = wv;
     const uint32_t c = ln >> 1;                    // signature of the pair
     const uint32_t i = base + c;
-    uint32_t kw[REC_WORDS];
-    {
-      StdIn xs = {};
-      key_words(i, kw, xs);
-    }
     ge q;
-    {
-      fe w;
-      uint32_t pflags;
-      const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
-      fe xw, ww;  // Q' = (x w, w^2) on E_w
-      fe_mul(xw, q.x, w);
-      fe_sqr(ww, w);
-      q.x = xw;
-      q.y = ww;
-      if (!pk) ge_set_g(q);  // dummy point (the lane is invalid: its digits are zero)
-    }
-    // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale
-    // Zg (both lanes of the pair build it; each keeps its coordinate in LDS) ----
+    key_point<STD>(i, n, recs, sa, q);
+    // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
     fe Zg;
-    {
-      gej p2, pj;
-      gej_set_ge(p2, q);
-      gej_double(p2, p2);  // 2Q (Jacobian, scale Z2)
-      fe z2, qx, qy;       // Q' = phi_Z2(Q) = (x Z2^2, y Z2^3)
-      fe_sqr(z2, p2.z);
-      fe_mul(qx, q.x, z2);
-      fe_mul(z2, z2, p2.z);
-      fe_mul(qy, q.y, z2);
-      qtab_store(qs, n_lanes, qlane, 0, 0, qx);
-      qtab_store(qs, n_lanes, qlane, 0, 2, qy);
-      qtab_store(qs, n_lanes, qlane, 1, 0, p2.x);
-      qtab_store(qs, n_lanes, qlane, 1, 2, p2.y);
-      pj.x = p2.x;
-      pj.y = p2.y;
-      fe_set_u32(pj.z, 1);
-#pragma unroll 1
-      for (int j = 2; j < QTAB_ENTRIES; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
-        bool hz, rz;
-        fe h;
-        gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
-        qtab_store(qs, n_lanes, qlane, j, 0, pj.x);
-        qtab_store(qs, n_lanes, qlane, j, 2, pj.y);
-        qtab_store(qs, n_lanes, qlane, (j - 1), 4, h);
-      }
-      fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
-      fe beta;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) beta.v[k] = FE_BETA[k];
-      auto put = [&](int j, const fe& x, const fe& y) {
-        fe v;
-        fe_sel(v, x, y, odd);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) qlds[half][j][k][ln] = v.v[k];
-      };
-      {
-        fe bx = pj.x;
-        if (half) fe_mul(bx, pj.x, beta);
-        put(QTAB_ENTRIES - 1, bx, pj.y);
-      }
-      fe rho;
-      fe_set_u32(rho, 1);
-#pragma unroll 1
-      for (int j = QTAB_ENTRIES - 2; j >= 0; --j) {
-        fe x, y, t;
-        if (j >= 1) {
-          qtab_load(qs, n_lanes, qlane, j, 4, t);  // H_{j+1}
-          fe_mul(rho, rho, t);
-        }
-        qtab_load(qs, n_lanes, qlane, j, 0, x);
-        qtab_load(qs, n_lanes, qlane, j, 2, y);
-        fe_sqr(t, rho);
-        fe_mul(x, x, t);
-        fe_mul(t, t, rho);
-        fe_mul(y, y, t);
-        if (half) fe_mul(x, x, beta);
-        put(j, x, y);
-      }
-    }
+    pair_table(q, half, odd, qs, n_lanes, qlane, qlds[half], ln, Zg);
     mark(half ? STAMP_TABLE1 : STAMP_TABLE0);
     __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
     if (half == 0) mark(STAMP_P);
@@ -926,47 +1046,12 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
 
     // ---- the chain: 33 radix-16 windows, pair form ----
     fe P, Z;
-    bool inf = true;
-    fe_set_zero(P);
-    fe_set_zero(Z);
-    uint32_t dw = valid ? im[(size_t)(IM_DIG + NWIN - 1) * n_pad + i] : DIG_ZERO;
-#pragma unroll 1
-    for (int win = NWIN - 1; win >= 0; --win) {
-      const int dg = half ? (int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS : (int)(dw & QDIG_MASK) - QBIAS;
-      const int mg = dg < 0 ? -dg : dg;
-      const int ie = mg ? mg - 1 : 0;
-      const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
-      if (win != NWIN - 1) {
-#pragma unroll 1
-        for (int d = 0; d < QW; ++d) {
-          if (!inf) pair_double(P, Z, odd);
-        }
-      }
-      const bool take = dg != 0;
-      const bool neg = (dg < 0) != negh;
-      fe T;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) T.v[k] = qlds[half][ie][k][ln];
-      fe_cneg(T, T, neg && odd);  // y -> -y on the odd lane
-      const bool was_inf = inf;
-      pair_accumulate(P, Z, inf, T, take, odd);
-      if (__any(take && was_inf)) pair_accumulate_from_inf(P, Z, inf, T, take && was_inf);
-      dw = dw_next;
-    }
+    bool inf;
+    pair_chain(P, Z, inf, qlds[half], im, n_pad, i, valid, negh, half, odd, ln, NWIN - 1, 0);
 
     mark(half ? STAMP_CHAIN1 : STAMP_CHAIN0);
     // ---- join: half 1's sum to half 0 through LDS ----
-    if (half == 1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (!odd) xch[k * PAIR_SIGS + c] = P.v[k];
-        else {
-          xch[(8 + k) * PAIR_SIGS + c] = P.v[k];
-          xch[(16 + k) * PAIR_SIGS + c] = Z.v[k];
-        }
-      }
-      if (odd) xch[24 * PAIR_SIGS + c] = inf ? 1u : 0u;
-    }
+    if (half == 1) pair_publish(xch, PAIR_SIGS, c, P, Z, inf, odd);
     fe Y, Zx;
     fe_xch(Y, P);   // even lane: Y of the pair
     fe_xch(Zx, Z);  // even lane: Z of the pair
@@ -978,28 +1063,14 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
       acc.x = P;
       acc.y = Y;
       acc.z = Zx;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        b.x.v[k] = xch[k * PAIR_SIGS + c];
-        b.y.v[k] = xch[(8 + k) * PAIR_SIGS + c];
-        b.z.v[k] = xch[(16 + k) * PAIR_SIGS + c];
-      }
-      const bool binf = xch[24 * PAIR_SIGS + c] != 0;
+      bool binf;
+      xch_read(xch, PAIR_SIGS, c, b, binf);
       gej_add_var(acc, inf, b, binf);  // B' = u2 Q' on E_w (iso scale Zg)
       gej A;
       fe y0;
-      uint32_t r[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        A.x.v[k] = aux[(size_t)(AUX_AX + k) * n_pad + i];
-        A.y.v[k] = aux[(size_t)(AUX_AX + 8 + k) * n_pad + i];
-        A.z.v[k] = aux[(size_t)(AUX_AX + 16 + k) * n_pad + i];
-        y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
-        r[k] = im[(size_t)(IM_R + k) * n_pad + i];
-      }
-      const uint32_t af = aux[(size_t)AUX_FLAGS * n_pad + i];
-      const bool ainf = (af & AUXF_AINF) != 0;
-      const bool is_sq = aux[(size_t)AUX_SQ * n_pad + i] != 0;
+      uint32_t r[8], af;
+      bool is_sq;
+      join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
       // B = phi^-1(B') = (X, Y, Z Zg y0) on E, R = A + B exactly, x compare
       gej bb;
       bb.x = acc.x;
@@ -1007,7 +1078,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
       fe zt;
       fe_mul(zt, acc.z, Zg);
       fe_mul(bb.z, zt, y0);
-      bool rinf = ainf;
+      bool rinf = (af & AUXF_AINF) != 0;
       gej_add_var(A, rinf, bb, inf);
       accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r) && (!STD || (af & AUXF_STDOK));
     }
@@ -1018,6 +1089,197 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
       if (wi < n_words) bits[wi] = even_bits(ball);
     }
     __syncthreads();  // barrier B: the next group's writers of xch / aux wait for the readers
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 2d. Block kernel (a block: at most BLK_SIGS signatures per CU). In the
+//     pair kernel one signature's chain is the latency: 128 doublings and 33
+//     additions of one pair of lanes, started only once the signature is
+//     parsed (the digits). Here the radix-16 windows are split at BLK_K:
+//       wave 0: windows 0..BLK_K-1 against the table of Q' (lanes 0-31 k1,
+//               lanes 32-63 k2), then S_lo = their sum and T = A + S_lo on E;
+//       wave 1: first Q4 = 2^(4 BLK_K) Q' by 4 BLK_K pair doublings from
+//               t = 0 (no digits needed), then the table of Q4 and windows
+//               BLK_K..NWIN-1 against it (lanes 0-31 k1, 32-63 k2), then
+//               S_hi, R = T + S_hi on E, the x compare and the verdicts;
+//       wave 2: the signature (lanes 0-15), then u1 * G (STD: the hashes);
+//       wave 3: the key's y0 = sqrt(w) (lanes 0-15).
+//     The doublings on wave 1's path stay 128, but only NWIN - BLK_K of the
+//     additions lie on it and the signature parse is hidden behind Q4.
+//     16 signatures per workgroup of 4 waves (one per SIMD): a 4,000-input
+//     block fills 250 CUs. The hand-offs are LDS flags (release / acquire at
+//     workgroup scope) instead of workgroup barriers, so no wave waits at a
+//     barrier for a phase it does not need.
+// ---------------------------------------------------------------------------
+#ifndef HKV_BLK_K
+#define HKV_BLK_K 23
+#endif
+constexpr int BLK_K = HKV_BLK_K;
+static_assert(BLK_K >= 2 && BLK_K <= NWIN - 2, "both chains take windows");
+constexpr int BLK_SIGS = 16;
+constexpr int BLK_TPB = 256;
+enum : int { BF_SIG = 0, BF_A = 1, BF_Y = 2, BF_T = 3, BF_COUNT = 4 };
+// publish: every prior write of the wave (LDS and global) before the flag
+HKV_DEV void blk_post(uint32_t* f, uint32_t seq) {
+  __threadfence_block();
+  __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+HKV_DEV void blk_wait(uint32_t* f, uint32_t seq) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq) __builtin_amdgcn_s_sleep(1);
+}
+// lanes of one wave exchanged data through LDS: the writes before the reads
+HKV_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool STD>
+__global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
+                                                               const uint32_t* __restrict__ gtab,
+                                                               uint32_t* __restrict__ qs,
+                                                               uint32_t* __restrict__ bits, uint32_t n_words,
+                                                               uint32_t* __restrict__ aux,
+                                                               uint32_t* __restrict__ recs, uint32_t mode,
+                                                               unsigned long long* __restrict__ clk, StdArgs sa) {
+  __shared__ QLane qlds[2];
+  __shared__ uint32_t xch[3][25 * BLK_SIGS];  // k2 -> k1 of wave 0, of wave 1; T wave 0 -> wave 1
+  __shared__ uint32_t shabuf[STD ? 16 * WG : 1];
+  __shared__ uint32_t bflag[BF_COUNT];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ln = threadIdx.x & 63;
+  const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
+  const uint32_t n_lanes = gridDim.x * 128u;
+  const uint32_t qlane = blockIdx.x * 128u + (threadIdx.x & 127u);
+  const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
+  auto mark = [&](int slot) {
+    if (stamp) clk[4 + slot] = wall_clock64();
+  };
+  if (threadIdx.x < BF_COUNT) bflag[threadIdx.x] = 0;
+  __syncthreads();
+  if (wv == 0) mark(STAMP_START);
+
+  uint32_t seq = 0;
+  for (uint32_t base = blockIdx.x * BLK_SIGS; base < n_pad; base += gridDim.x * BLK_SIGS) {
+    ++seq;
+    if (wv == 2) {
+      const uint32_t i = base + ln;
+      const bool on = ln < BLK_SIGS;
+      uint32_t flags;
+      bool use;
+      sc sinv, m;
+      StdIn x = {};
+      sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags);
+      blk_post(&bflag[BF_SIG], seq);
+      mark(STAMP_SIG);
+      sig_wave_gsum<STD>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
+      blk_post(&bflag[BF_A], seq);
+      mark(STAMP_GSUM);
+    } else if (wv == 3) {
+      if (ln < BLK_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
+      blk_post(&bflag[BF_Y], seq);
+      mark(STAMP_SQRT);
+    } else {
+      // ---- chain waves: lanes 0-31 k1, 32-63 k2 (two lanes per chain) ----
+      const int half = (int)(ln >> 5);
+      const uint32_t c = (ln & 31u) >> 1;
+      const uint32_t i = base + c;
+      ge q;
+      key_point<STD>(i, n, recs, sa, q);
+      fe Zg, z4;
+      if (wv == 0) {
+        fe_set_u32(z4, 1);
+        pair_table(q, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
+        mark(STAMP_TABLE0);
+      } else {
+        // Q4 = 2^(4 BLK_K) Q' (Jacobian, its Z on the odd lane), then q = (X4, Y4)
+        // as an affine point of the isomorphic curve of scale Z4
+        fe P, Z;
+        fe_sel(P, q.x, q.y, odd);
+        fe_set_u32(Z, 1);
+#pragma unroll 1
+        for (int d = 0; d < QW * BLK_K; ++d) pair_double(P, Z, odd);
+        fe_bc0(q.x, P);
+        fe_bc1(q.y, P);
+        fe_bc1(z4, Z);
+        pair_table(q, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
+        mark(STAMP_TABLE1);
+      }
+      blk_wait(&bflag[BF_SIG], seq);  // the digits, r and flags are in im
+      if (wv == 0) mark(STAMP_P);
+      const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+      const bool valid = (i < n) && (flags & FLAG_VALID);
+      const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
+      fe P, Z;
+      bool inf;
+      if (wv == 0) pair_chain(P, Z, inf, qlds[0], im, n_pad, i, valid, negh, half, odd, ln, BLK_K - 1, 0);
+      else pair_chain(P, Z, inf, qlds[1], im, n_pad, i, valid, negh, half, odd, ln, NWIN - 1, BLK_K);
+      mark(wv == 0 ? STAMP_CHAIN0 : STAMP_CHAIN1);
+      // ---- k2's part to k1's lanes (same wave), S = k1 part + k2 part ----
+      uint32_t* xk = xch[wv];
+      if (half == 1) pair_publish(xk, BLK_SIGS, c, P, Z, inf, odd);
+      fe Y, Zx;
+      fe_xch(Y, P);   // even lane: Y of the pair
+      fe_xch(Zx, Z);  // even lane: Z of the pair
+      wave_lds_sync();
+      gej S;
+      S.x = P;
+      S.y = Y;
+      S.z = Zx;
+      bool sinf = inf;
+      if (half == 0) {
+        gej b;
+        bool binf;
+        xch_read(xk, BLK_SIGS, c, b, binf);
+        gej_add_var(S, sinf, b, binf);  // on E_w at iso scale Zg * z4
+      }
+      if (wv == 0) {
+        // ---- T = A + phi^-1(S_lo) on E (A = u1 G, y0 the key's y) ----
+        blk_wait(&bflag[BF_A], seq);
+        blk_wait(&bflag[BF_Y], seq);
+        mark(STAMP_A);
+        if (half == 0) {
+          gej A;
+          fe y0;
+          uint32_t r[8], af;
+          bool is_sq;
+          join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
+          fe zt;
+          fe_mul(zt, S.z, Zg);
+          fe_mul(S.z, zt, y0);
+          bool tinf = (af & AUXF_AINF) != 0;
+          gej_add_var(A, tinf, S, sinf);
+          if (!odd) xch_write(xch[2], BLK_SIGS, c, A, tinf);
+        }
+        blk_post(&bflag[BF_T], seq);
+      } else {
+        // ---- R = T + phi^-1(S_hi) on E, the x compare, the verdicts ----
+        blk_wait(&bflag[BF_T], seq);
+        bool accept = false;
+        if (half == 0) {
+          gej A, T;
+          fe y0;
+          uint32_t r[8], af;
+          bool is_sq, tinf;
+          join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
+          xch_read(xch[2], BLK_SIGS, c, T, tinf);
+          fe zt;
+          fe_mul(zt, S.z, Zg);
+          fe_mul(zt, zt, z4);
+          fe_mul(S.z, zt, y0);
+          gej_add_var(T, tinf, S, sinf);
+          accept = valid && is_sq && !tinf && x_matches_r(T.x, T.z, r) && (!STD || (af & AUXF_STDOK));
+        }
+        const uint64_t ball = __ballot(accept && !odd);
+        mark(STAMP_JOIN);
+        if (ln == 0) {
+          const uint32_t wi = base / 32;
+          if (wi < n_words) reinterpret_cast<uint16_t*>(bits)[base / BLK_SIGS] = (uint16_t)(even_bits(ball) & 0xFFFFu);
+        }
+      }
+    }
+    __syncthreads();  // the group's LDS (tables, exchanges, flags' data) is read before the next group's writes
   }
 }
 
@@ -1759,16 +2021,22 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
   hipLaunchKernelGGL(hkv_glv_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n_pad, im);
   return hipGetLastError();
 }
-// split: small batches (hkv_pair_split_kernel, PAIR_SIGS signatures per
-// workgroup, no separate prologue); mid: full-grid batches of at most 2 waves
-// per SIMD, the paired-form instance at a 2-wave register allocation
+// split: small batches — at most BLK_SIGS signatures per CU (a block) the
+// block kernel, else hkv_pair_split_kernel (PAIR_SIGS signatures per
+// workgroup); no separate prologue. mid: full-grid batches of at most 2
+// waves per SIMD, the paired-form instance at a 2-wave register allocation
+static inline bool block_batch(uint32_t n_pad, uint32_t n_cu) { return n_pad <= (uint32_t)BLK_SIGS * n_cu; }
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool mid,
-                         unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, hipStream_t st) {
-  if (split)
+                         unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, uint32_t n_cu,
+                         hipStream_t st) {
+  uint32_t* rw = const_cast<uint32_t*>((const uint32_t*)recs);
+  if (split && block_batch(n_pad, n_cu))
+    hipLaunchKernelGGL(hkv_block_kernel<false>, dim3(n_pad / BLK_SIGS), dim3(BLK_TPB), 0, st, im, n, n_pad, gtab, qs,
+                       bits, n_words, aux, rw, mode, clk, StdArgs{});
+  else if (split)
     hipLaunchKernelGGL(hkv_pair_split_kernel<false>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, aux, const_cast<uint32_t*>((const uint32_t*)recs), mode, clk,
-                       StdArgs{});
+                       gtab, qs, bits, n_words, aux, rw, mode, clk, StdArgs{});
   else if (mid)
     hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
   else
@@ -1776,16 +2044,21 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
   return hipGetLastError();
 }
 // small batches of standard inputs: parse, the Q chains, the script checks,
-// the sighash and the verdict in one launch (hkv_pair_split_kernel<true>);
-// txt must hold the batch's tx index rows and BIP143 hashes
+// the sighash and the verdict in one launch (hkv_block_kernel<true> or
+// hkv_pair_split_kernel<true>); txt must hold the batch's tx index rows
 hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
-                                   hipStream_t st) {
+                                   uint32_t n_cu, hipStream_t st) {
   const StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid};
-  hipLaunchKernelGGL(hkv_pair_split_kernel<true>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad, gtab,
-                     qs, bits, n_words, aux, reinterpret_cast<uint32_t*>(recs), (uint32_t)HKV_MODE_HASKOIN, clk, sa);
+  uint32_t* rw = reinterpret_cast<uint32_t*>(recs);
+  if (block_batch(n_pad, n_cu))
+    hipLaunchKernelGGL(hkv_block_kernel<true>, dim3(n_pad / BLK_SIGS), dim3(BLK_TPB), 0, st, im, n, n_pad, gtab, qs,
+                       bits, n_words, aux, rw, (uint32_t)HKV_MODE_HASKOIN, clk, sa);
+  else
+    hipLaunchKernelGGL(hkv_pair_split_kernel<true>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
+                       gtab, qs, bits, n_words, aux, rw, (uint32_t)HKV_MODE_HASKOIN, clk, sa);
   return hipGetLastError();
 }
 hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {

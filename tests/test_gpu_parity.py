@@ -388,22 +388,27 @@ def test_config5_ibd_16m_sharded_bitmap(torch, ver, coracle):
 
 
 def test_split_lane_ecmult_matches_full_grid(torch, ver, coracle):
-    """Small batches run the small-batch kernel (hkv_pair_split_kernel<false>:
-    k1 and k2 chains on their own waves, two lanes per chain; chosen when the
-    padded batch fills at most an eighth of the resident grid, 32,768
-    signatures on an MI355X); large ones one lane per signature
-    (hkv_ecmult_kernel + the finish kernels). The same adversarial records verified in
-    both launch shapes give identical verdicts, equal to the C oracle on a
-    slice, in both modes."""
+    """Three launch shapes on the same adversarial records: at most 16
+    signatures per CU (4,096 on an MI355X) the block kernel
+    (hkv_block_kernel<false>: each chain's windows split between the table of
+    Q' and that of 2^92 Q'); up to an eighth of the resident grid (32,768)
+    the pair kernel (hkv_pair_split_kernel<false>: k1 and k2 chains on their
+    own waves, two lanes per chain); above it one lane per signature
+    (hkv_ecmult_kernel + the finish kernels). Identical verdicts, equal to
+    the labels and to the C oracle on a slice, in both modes; the block
+    shape also at a size that is not a multiple of 16 or 32."""
     from hkv import adversarial
-    n_small, n_big = 1 << 15, (1 << 15) + 257          # n_pad 32,768 (split) / 33,024 (full)
+    n_blk, n_small, n_big = 1 << 12, 1 << 15, (1 << 15) + 257   # block / pair (32,768) / full grid (33,024)
     d = gen_device(torch, ver, n_big, seed=0x53504C54)
     adv, lab_lib, lab_hask, _ = adversarial.mutate(d.cpu().numpy(), seed=0x53504C54)
     d.copy_(torch.from_numpy(adv))
     for mode, lab in ((0, lab_lib), (1, lab_hask)):
+        blk = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n_blk, mode), n_blk)
+        odd = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n_blk - 37, mode), n_blk - 37)
         small = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n_small, mode), n_small)
         big = adversarial.unpack_bits(verify_dev_bits(torch, ver, d, n_big, mode), n_big)
         assert (small == big[:n_small]).all()
+        assert (blk == big[:n_blk]).all() and (odd == big[:n_blk - 37]).all()
         assert (big == lab).all() and (small == lab[:n_small]).all()
         exp = oracle_batch(coracle, adv[: 8192 * 168].tobytes(), mode, threads=16)
         assert (small[:8192] == exp).all()
