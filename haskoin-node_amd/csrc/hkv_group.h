@@ -309,6 +309,44 @@ HKV_DEV void pair_accumulate(fe& P, fe& Z, bool& inf, const fe& TXY, bool take, 
     inf = inf || (degen && !rz);               // T == -acc
   }
 }
+// P += TXY in place for a table build: TXY affine on the curve of the
+// accumulator's Jacobian scale, P finite and never +-TXY (the multiples
+// j Q, j < 9, of a point of prime order). Returns the z-ratio H = U2 - X1
+// on the even lane (Z3 = Z1 H). The live branch of pair_accumulate.
+HKV_DEV void pair_add_affine(fe& P, fe& Z, const fe& TXY, uint32_t odd, fe& H) {
+  fe z2, O1, O2, R2, R3, Rr, R5, R6, W, X3, D, R7, t;
+  fe_sqr(z2, Z);              //                | Z^2
+  fe_bc1(O2, z2);             // Z^2            | Z^2
+  fe_sel(O1, TXY, Z, odd);    // tx             | Z
+  fe_mul(R2, O1, O2);         // U2 = tx Z^2    | Z^3
+  fe_sub(H, R2, P);           // H = U2 - X1
+  fe_sel(O1, H, TXY, odd);    // H              | ty
+  fe_sel(O2, H, R2, odd);     // H              | Z^3
+  fe_mul(R3, O1, O2);         // H^2            | S2 = ty Z^3
+  fe_sub(Rr, R3, P);          //                | R = S2 - Y1
+  fe_sel(O1, H, Rr, odd);     // H              | R
+  fe_sel(O2, R3, Rr, odd);    // H^2            | R
+  fe_mul(R5, O1, O2);         // H^3            | R^2
+  fe_xch(t, H);               //                | H
+  fe_sel(O1, P, Z, odd);      // X1             | Z1
+  fe_sel(O2, R3, t, odd);     // H^2            | H
+  fe_mul(R6, O1, O2);         // V = X1 H^2     | Z3 = Z1 H
+  fe_xch(W, R5);              // R^2            | H^3
+  fe_sub(X3, W, R5);
+  fe_shl(t, R6, 1);
+  fe_sub(X3, X3, t);          // X3 = R^2 - H^3 - 2V
+  fe_sub(D, R6, X3);          // V - X3
+  fe_xch(t, D);               //                | V - X3
+  fe_xch(O1, P);              // Y1             | X1
+  fe_sel(O1, O1, Rr, odd);    // Y1             | R
+  fe_sel(O2, R5, t, odd);     // H^3            | V - X3
+  fe_mul(R7, O1, O2);         // Y1 H^3         | R (V - X3)
+  fe_xch(t, R7);
+  fe_sub(t, R7, t);           //                | Y3 = R (V - X3) - Y1 H^3
+  fe_sel(P, X3, t, odd);
+  Z = R6;                     //                | Z3
+}
+
 // (P, Z) := (TXY, 1) on pairs that take a point while at infinity
 HKV_DEV void pair_accumulate_from_inf(fe& P, fe& Z, bool& inf, const fe& TXY, bool take) {
   const bool f = take && inf;

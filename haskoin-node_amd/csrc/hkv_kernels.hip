@@ -697,68 +697,71 @@ struct StdArgs {
 // even lane; y on the odd lane).
 typedef uint32_t QLane[QTAB_ENTRIES][8][64];
 
-// j * q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg (q affine
-// on its own curve; the a = 0 formulas never use b). Both lanes of a pair
-// build it; entries stream through the lane's qs scratch, then the backward
-// rescale writes the LDS table. Returns Zg.
-HKV_DEV void pair_table(const ge& q, int half, uint32_t odd, uint32_t* __restrict__ qs, uint32_t n_lanes,
+// j * q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg, in pair
+// form: Q = x | y is affine on its own curve (the a = 0 formulas never use
+// b). Forward: 2Q, Q' = phi_Z2(Q), P_{j+1} = P_j + Q' (pair additions; each
+// lane streams its coordinate and the z-ratio H_{j+1} to the lane's qs
+// scratch); backward: rho_j = prod_{k>j} H_k, entry j = (x rho^2, y rho^3)
+// (beta * x on the half-1 even lanes) straight into the LDS table — four
+// product levels per entry (rho H, rho^2, [x beta | rho^3], [. t | y rho^3])
+// instead of six one-lane products. Returns Zg on both lanes.
+HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, uint32_t* __restrict__ qs, uint32_t n_lanes,
                         uint32_t qlane, QLane& ql, uint32_t ln, fe& Zg) {
-  gej p2, pj;
-  gej_set_ge(p2, q);
-  gej_double(p2, p2);  // 2Q (Jacobian, scale Z2)
-  fe z2, qx, qy;       // Q' = phi_Z2(Q) = (x Z2^2, y Z2^3)
-  fe_sqr(z2, p2.z);
-  fe_mul(qx, q.x, z2);
-  fe_mul(z2, z2, p2.z);
-  fe_mul(qy, q.y, z2);
-  qtab_store(qs, n_lanes, qlane, 0, 0, qx);
-  qtab_store(qs, n_lanes, qlane, 0, 2, qy);
-  qtab_store(qs, n_lanes, qlane, 1, 0, p2.x);
-  qtab_store(qs, n_lanes, qlane, 1, 2, p2.y);
-  pj.x = p2.x;
-  pj.y = p2.y;
-  fe_set_u32(pj.z, 1);
+  const uint32_t plane = qlane & ~1u;  // the pair's even lane (its H slots)
+  fe P = Q, Z, O1, O2, zz, zs, R, Qp;
+  fe_set_u32(Z, 1);
+  pair_double(P, Z, odd);     // 2Q = X2 | Y2, Z2 on the odd lane
+  fe_bc1(zz, Z);              // Z2             | Z2
+  fe_sqr(zs, zz);             // Z2^2
+  fe_sel(O1, Q, zz, odd);     // x              | Z2
+  fe_mul(R, O1, zs);          // x Z2^2         | Z2^3
+  fe_mul(O2, Q, R);           //                | y Z2^3
+  fe_sel(Qp, R, O2, odd);     // Q' = phi_Z2(Q): x Z2^2 | y Z2^3
+  qtab_store(qs, n_lanes, qlane, 0, 0, Qp);
+  qtab_store(qs, n_lanes, qlane, 1, 0, P);
+  fe_set_u32(Z, 1);           // P_2 = (X2, Y2, 1) on the curve of scale Z2
 #pragma unroll 1
-  for (int j = 2; j < QTAB_ENTRIES; ++j) {  // P_{j+1} = P_j + Q' (mixed, never degenerate)
-    bool hz, rz;
-    fe h;
-    gej_add_ge_core(pj, pj, pj.z, qx, qy, hz, rz, &h);
-    qtab_store(qs, n_lanes, qlane, j, 0, pj.x);
-    qtab_store(qs, n_lanes, qlane, j, 2, pj.y);
-    qtab_store(qs, n_lanes, qlane, (j - 1), 4, h);
+  for (int j = 2; j < QTAB_ENTRIES; ++j) {
+    fe H;
+    pair_add_affine(P, Z, Qp, odd, H);
+    qtab_store(qs, n_lanes, qlane, j, 0, P);
+    if (!odd) qtab_store(qs, n_lanes, qlane, j - 1, 2, H);  // H_{j+1}
   }
-  fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
-  fe beta;
+  __threadfence_block();      // the even lanes' H stores before the odd lanes' loads
+  fe zc;
+  fe_bc1(zc, Z);
+  fe_mul(Zg, zz, zc);         // total scale: phi_Z2 then phi_Zc
+  fe beta, one;
 #pragma unroll
   for (int k = 0; k < 8; ++k) beta.v[k] = FE_BETA[k];
-  auto put = [&](int j, const fe& x, const fe& y) {
-    fe v;
-    fe_sel(v, x, y, odd);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ql[j][k][ln] = v.v[k];
-  };
+  fe_set_u32(one, 1);
+  fe bsel;                    // the even lane's x factor: beta (half 1) or 1
+  fe_sel(bsel, half ? beta : one, one, odd);
   {
-    fe bx = pj.x;
-    if (half) fe_mul(bx, pj.x, beta);
-    put(QTAB_ENTRIES - 1, bx, pj.y);
+    fe bx;
+    fe_mul(bx, P, bsel);      // beta x | y (x 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ql[QTAB_ENTRIES - 1][k][ln] = bx.v[k];
   }
   fe rho;
   fe_set_u32(rho, 1);
 #pragma unroll 1
   for (int j = QTAB_ENTRIES - 2; j >= 0; --j) {
-    fe x, y, t;
+    fe c, t, h;
     if (j >= 1) {
-      qtab_load(qs, n_lanes, qlane, j, 4, t);  // H_{j+1}
-      fe_mul(rho, rho, t);
+      qtab_load(qs, n_lanes, plane, j, 2, h);  // H_{j+1}
+      fe_mul(rho, rho, h);
     }
-    qtab_load(qs, n_lanes, qlane, j, 0, x);
-    qtab_load(qs, n_lanes, qlane, j, 2, y);
-    fe_sqr(t, rho);
-    fe_mul(x, x, t);
-    fe_mul(t, t, rho);
-    fe_mul(y, y, t);
-    if (half) fe_mul(x, x, beta);
-    put(j, x, y);
+    qtab_load(qs, n_lanes, qlane, j, 0, c);    // x | y of entry j
+    fe_sqr(t, rho);                            // rho^2
+    fe_sel(O1, c, t, odd);                     // x              | rho^2
+    fe_sel(O2, bsel, rho, odd);                // beta or 1      | rho
+    fe_mul(R, O1, O2);                         // beta x         | rho^3
+    fe_sel(O1, R, c, odd);                     // beta x         | y
+    fe_sel(O2, t, R, odd);                     // rho^2          | rho^3
+    fe_mul(R, O1, O2);                         // beta x rho^2   | y rho^3
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ql[j][k][ln] = R.v[k];
   }
 }
 
@@ -1035,8 +1038,9 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
     ge q;
     key_point<STD>(i, n, recs, sa, q);
     // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
-    fe Zg;
-    pair_table(q, half, odd, qs, n_lanes, qlane, qlds[half], ln, Zg);
+    fe Zg, Qxy;
+    fe_sel(Qxy, q.x, q.y, odd);
+    pair_table(Qxy, half, odd, qs, n_lanes, qlane, qlds[half], ln, Zg);
     mark(half ? STAMP_TABLE1 : STAMP_TABLE0);
     __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
     if (half == 0) mark(STAMP_P);
@@ -1187,23 +1191,20 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       const uint32_t i = base + c;
       ge q;
       key_point<STD>(i, n, recs, sa, q);
-      fe Zg, z4;
+      fe Zg, z4, P, Z;
+      fe_sel(P, q.x, q.y, odd);
       if (wv == 0) {
         fe_set_u32(z4, 1);
-        pair_table(q, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
+        pair_table(P, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
         mark(STAMP_TABLE0);
       } else {
-        // Q4 = 2^(4 BLK_K) Q' (Jacobian, its Z on the odd lane), then q = (X4, Y4)
-        // as an affine point of the isomorphic curve of scale Z4
-        fe P, Z;
-        fe_sel(P, q.x, q.y, odd);
+        // Q4 = 2^(4 BLK_K) Q' = X4 | Y4 with Z4 on the odd lane: (X4, Y4) is
+        // an affine point of the isomorphic curve of scale Z4
         fe_set_u32(Z, 1);
 #pragma unroll 1
         for (int d = 0; d < QW * BLK_K; ++d) pair_double(P, Z, odd);
-        fe_bc0(q.x, P);
-        fe_bc1(q.y, P);
         fe_bc1(z4, Z);
-        pair_table(q, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
+        pair_table(P, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
         mark(STAMP_TABLE1);
       }
       blk_wait(&bflag[BF_SIG], seq);  // the digits, r and flags are in im
@@ -1211,7 +1212,6 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
       const bool valid = (i < n) && (flags & FLAG_VALID);
       const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
-      fe P, Z;
       bool inf;
       if (wv == 0) pair_chain(P, Z, inf, qlds[0], im, n_pad, i, valid, negh, half, odd, ln, BLK_K - 1, 0);
       else pair_chain(P, Z, inf, qlds[1], im, n_pad, i, valid, negh, half, odd, ln, NWIN - 1, BLK_K);
