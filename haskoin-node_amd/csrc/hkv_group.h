@@ -309,6 +309,44 @@ HKV_DEV void pair_accumulate(fe& P, fe& Z, bool& inf, const fe& TXY, bool take, 
     inf = inf || (degen && !rz);               // T == -acc
   }
 }
+// ---- quad-lane form: one point on four lanes (4c .. 4c + 3) ----
+// V = X | Y | Z | (unused) on quad lanes 0..3. A doubling is S + 2M deep:
+// [X^2 | Y^2], then [X B | B^2 | Y Z | E'^2] on all four lanes, then
+// [E'(M - X3')] — against 2S + 2M in the pair form. Operands move by DPP
+// quad permutations (quad_perm [s0, s1, s2, s3]: lane q reads lane s_q of
+// its quad) and lane-mask selects (m0, m1, m2: all ones on quad lane 0, 1, 2).
+template <int PERM>
+HKV_DEV void fe_quad(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], PERM, 0xF, 0xF, false);
+}
+constexpr int QP_0 = 0x00, QP_1 = 0x55, QP_3 = 0xFF, QP_0112 = 0xD4;  // [0,0,0,0] [1,1,1,1] [3,3,3,3] [0,1,1,3]
+// 2V in the halved form of gej_double (the same point scaled by 1/2)
+HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
+  fe R1, Bq, Aq, E, T, opA, opB, R2, Mq, Cq, E2q, t, X3, D, Y3;
+  fe_sqr(R1, V);              // A = X^2 | B = Y^2 | . | .
+  fe_quad<QP_1>(Bq, R1);      // B on every lane
+  fe_quad<QP_0>(Aq, R1);      // A on every lane
+  fe_mul_small(E, Aq, 3);
+  fe_half(E, E);              // E' = 3A/2
+  fe_quad<QP_0112>(T, V);     // X | . | Y | .
+  fe_sel(opA, E, Bq, m1);
+  fe_sel(opA, opA, T, m0 | m2);   // X | B | Y | E'
+  fe_sel(opB, E, V, m2);
+  fe_sel(opB, opB, Bq, m0 | m1);  // B | B | Z | E'
+  fe_mul(R2, opA, opB);       // M = X B | C = B^2 | Z3' = Y Z | E'^2
+  fe_quad<QP_0>(Mq, R2);
+  fe_quad<QP_1>(Cq, R2);
+  fe_quad<QP_3>(E2q, R2);
+  fe_shl(t, Mq, 1);
+  fe_sub(X3, E2q, t);         // X3' = E'^2 - 2M
+  fe_sub(D, Mq, X3);          // M - X3'
+  fe_mul(t, E, D);
+  fe_sub(Y3, t, Cq);          // Y3' = E'(M - X3') - C
+  fe_sel(V, R2, Y3, m1);
+  fe_sel(V, V, X3, m0);       // X3' | Y3' | Z3' | .
+}
+
 // P += TXY in place for a table build: TXY affine on the curve of the
 // accumulator's Jacobian scale, P finite and never +-TXY (the multiples
 // j Q, j < 9, of a point of prime order). Returns the z-ratio H = U2 - X1

@@ -1189,21 +1189,35 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       const int half = (int)(ln >> 5);
       const uint32_t c = (ln & 31u) >> 1;
       const uint32_t i = base + c;
-      ge q;
-      key_point<STD>(i, n, recs, sa, q);
       fe Zg, z4, P, Z;
-      fe_sel(P, q.x, q.y, odd);
       if (wv == 0) {
+        ge q;
+        key_point<STD>(i, n, recs, sa, q);
+        fe_sel(P, q.x, q.y, odd);
         fe_set_u32(z4, 1);
         pair_table(P, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
         mark(STAMP_TABLE0);
       } else {
-        // Q4 = 2^(4 BLK_K) Q' = X4 | Y4 with Z4 on the odd lane: (X4, Y4) is
-        // an affine point of the isomorphic curve of scale Z4
-        fe_set_u32(Z, 1);
+        // Q4 = 2^(4 BLK_K) Q' on four lanes per signature (lanes 4c'..4c'+3,
+        // quad_double: S + 2M per doubling), then to the chains' pair layout:
+        // X4 | Y4 with Z4 on both lanes, (X4, Y4) an affine point of the
+        // isomorphic curve of scale Z4
+        const uint32_t cq = ln >> 2, qd = ln & 3u;
+        const uint32_t m0 = qd == 0 ? ~0u : 0u, m1 = qd == 1 ? ~0u : 0u, m2 = qd == 2 ? ~0u : 0u;
+        ge q;
+        key_point<STD>(base + cq, n, recs, sa, q);
+        fe V;
+        fe_set_u32(V, 1);
+        fe_sel(V, V, q.y, m1);
+        fe_sel(V, V, q.x, m0);  // x | y | 1 | 1
 #pragma unroll 1
-        for (int d = 0; d < QW * BLK_K; ++d) pair_double(P, Z, odd);
-        fe_bc1(z4, Z);
+        for (int d = 0; d < QW * BLK_K; ++d) quad_double(V, m0, m1, m2);
+        const int src_p = (int)(4 * c + (odd ? 1u : 0u)), src_z = (int)(4 * c + 2);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          P.v[k] = (uint32_t)__shfl((int)V.v[k], src_p);
+          z4.v[k] = (uint32_t)__shfl((int)V.v[k], src_z);
+        }
         pair_table(P, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
         mark(STAMP_TABLE1);
       }
