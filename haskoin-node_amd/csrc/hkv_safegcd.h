@@ -6,8 +6,8 @@
 // Replaces the Fermat chain a^(n-2) (≈ 255 squarings + 75 multiplications
 // mod n) used for s^-1 in secp256k1_ecdsa_sig_verify step (5) [dep; SURVEY.md
 // §8(a) a3]. The result is the same field element; only the cost changes:
-// 25 outer iterations × (30 branch-free divsteps on the low word, one 2×2
-// matrix applied to (f, g) and, mod n, to (d, e)).
+// 25 outer iterations × (30 divsteps on the low word, in libsecp256k1's
+// variable-time form, one 2×2 matrix applied to (f, g) and, mod n, to (d, e)).
 //
 // Bound: for odd f < 2^256 and 0 <= g < f, ⌊(49·256 + 80)/17⌋ = 742
 // divsteps (delta starting at 1) reach g = 0 (paper, Theorem 11.2); at most
@@ -71,37 +71,47 @@ HKV_HD void to30(int32_t r[9], const uint32_t a[8]) {
   r[8] = (int32_t)(a[7] >> 16);
 }
 
-// 30 divsteps on the low words of f and g; returns the transition matrix
-// (u, v, q, r) scaled by 2^30 and the updated delta.
-HKV_HD int32_t divsteps30(int32_t delta, uint32_t f, uint32_t g, int32_t t[4]) {
+HKV_HD int ctz32(uint32_t x) { return __builtin_ctz(x); }  // x != 0
+
+// 30 divsteps on the low words of f and g, in libsecp256k1's variable-time
+// form (secp256k1_modinv32_divsteps_30_var; eta = -delta): a run of even g
+// is one shift (count trailing zeros), and each odd g cancels up to
+// min(eta + 1, i, 8) low bits at once by adding w f, w = -g / f mod 2^8.
+// It is the same divstep sequence as the constant-time form, so the 742-step
+// bound holds; the inputs (signatures, keys) are public. Returns the
+// transition matrix (u, v, q, r) scaled by 2^30 and the updated eta.
+HKV_HD int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
-#pragma unroll
-  for (int i = 0; i < 30; ++i) {
-    // delta > 0 and g odd: (f, g, u, v, q, r, delta) <- (g, -f, q, r, -u, -v, -delta)
-    const uint32_t sw = (uint32_t)(-(int32_t)((delta > 0) & (int32_t)(g & 1u)));
-    const uint32_t f0 = f, u0 = u, v0 = v;
-    f = (g & sw) | (f & ~sw);
-    g = ((0u - f0) & sw) | (g & ~sw);
-    u = (q & sw) | (u & ~sw);
-    q = ((0u - u0) & sw) | (q & ~sw);
-    v = (r & sw) | (v & ~sw);
-    r = ((0u - v0) & sw) | (r & ~sw);
-    delta = (int32_t)(((uint32_t)(-delta) & sw) | ((uint32_t)delta & ~sw));
-    // g odd: g += f, q += u, r += v
-    const uint32_t od = 0u - (g & 1u);
-    g += f & od;
-    q += u & od;
-    r += v & od;
-    g >>= 1;
-    u <<= 1;
-    v <<= 1;
-    delta += 1;
+  int i = 30;
+  for (;;) {
+    const int zeros = ctz32(g | (0xFFFFFFFFu << i));  // the sentinel bit i stops the count
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {  // g odd and delta > 0: (f, g, u, v, q, r) <- (g, -f, q, r, -u, -v)
+      uint32_t tmp;
+      eta = -eta;
+      tmp = f; f = g; g = 0u - tmp;
+      tmp = u; u = q; q = 0u - tmp;
+      tmp = v; v = r; r = 0u - tmp;
+    }
+    const int limit = (eta + 1) > i ? i : (eta + 1);
+    const uint32_t m = (0xFFFFFFFFu >> (32 - limit)) & 255u;
+    uint32_t x = (3u * f) ^ 2u;  // f^-1 mod 2^5 (f odd)
+    x *= 2u - f * x;             // mod 2^10
+    const uint32_t w = (0u - g * x) & m;
+    g += f * w;
+    q += u * w;
+    r += v * w;
   }
   t[0] = (int32_t)u;
   t[1] = (int32_t)v;
   t[2] = (int32_t)q;
   t[3] = (int32_t)r;
-  return delta;
+  return eta;
 }
 
 // (f, g) <- t (f, g) / 2^30 (exact)
@@ -165,11 +175,11 @@ HKV_HD void inv_mod(uint32_t out[8], const uint32_t a[8]) {
   }
   e[0] = 1;
   to30(g, a);
-  int32_t delta = 1;
+  int32_t eta = -1;  // -delta
 #pragma unroll 1
   for (int it = 0; it < 25; ++it) {
     int32_t t[4];
-    delta = divsteps30(delta, (uint32_t)f[0] | ((uint32_t)f[1] << 30), (uint32_t)g[0] | ((uint32_t)g[1] << 30), t);
+    eta = divsteps30(eta, (uint32_t)f[0] | ((uint32_t)f[1] << 30), (uint32_t)g[0] | ((uint32_t)g[1] << 30), t);
     update_fg(f, g, t);
     update_de<M>(d, e, t);
 #if HKV_SGCD_EARLY
