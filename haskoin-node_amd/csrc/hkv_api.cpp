@@ -430,7 +430,7 @@ int wait_ms_total(DevCtx& d, hipStream_t st, uint64_t seq, uint64_t* total) {
 // <true>): the chains start from the parsed keys and signatures while the
 // signature wave computes the sighashes and script checks beside them.
 int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
-                             void* recs, uint32_t* out_bits, hipStream_t st) {
+                             void* recs, uint32_t* out_bits, const hkv::MsScan* ms, hipStream_t st) {
   const size_t n_pad = round_up(n, hkv::WG);
   int rc = ensure_dev_buffers(d, n_pad);
   if (!rc) rc = ensure_aux(d, n_pad, st);
@@ -444,7 +444,7 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
   HKV_TRY(hkv::launch_std_verify_split(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
                                        (uint32_t)n_pad, forkid, static_cast<uint8_t*>(recs), d.im, d.gtab, d.qs,
                                        d.aux, out_bits, (uint32_t)((n + 31) / 32), d.profile ? d.clk : nullptr,
-                                       (uint32_t)d.n_cu, st),
+                                       (uint32_t)d.n_cu, ms, st),
           "std-input verify launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
@@ -460,10 +460,10 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
   // it, off the block's critical path); larger ones: the extraction kernel,
   // then the record verify
   const bool fused = split_batch(d, n);
-  int rc = fused ? enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
-  if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, st);
-  if (rc) return rc;
-  rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
+  // the block kernel (at most 16 inputs per CU) runs the multisig scan on
+  // its square-root wave; otherwise the scan kernel follows the verify launch
+  const bool fused_scan = fused && hkv::std_split_scans((uint32_t)round_up(n, hkv::WG), (uint32_t)d.n_cu);
+  int rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
   if (!rc) rc = grow(&d.ms[2], &d.ms_cap[2], n * 8, "hipMalloc(multisig offsets)");
   if (rc) return rc;
   uint32_t* desc = static_cast<uint32_t*>(d.ms[0]);
@@ -476,9 +476,14 @@ int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job*
     d.ms_dirty = false;
   }
   d.ms_dirty = true;  // until this call has read the sum
-  HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
-                              desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq, st),
-          "multisig scan launch");
+  const hkv::MsScan ms{desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq};
+  rc = fused ? enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, fused_scan ? &ms : nullptr, st);
+  if (rc) return rc;
+  if (!fused_scan)
+    HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
+                                desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq, st),
+            "multisig scan launch");
   if (!fused) {
     rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
     if (rc) return rc;

@@ -32,11 +32,22 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, uint32_t n_cu,
                          hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
+// the multisig scan operands a fused launch may take over (hkv_ms_scan_kernel's)
+struct MsScan {
+  uint32_t* desc;
+  uint64_t* off;
+  uint64_t* counters;
+  uint64_t* host_total;
+  uint64_t seq;
+};
+// small batches of standard inputs in one launch; with ms, the block kernel
+// (std_split_scans) also runs the multisig scan
 hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
-                                   uint32_t n_cu, hipStream_t st);
+                                   uint32_t n_cu, const MsScan* ms, hipStream_t st);
+bool std_split_scans(uint32_t n_pad, uint32_t n_cu);
 // y-free full-grid batches: u1 * G, the y0 = num / den reduction and the verdict bitmap
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st);

@@ -689,6 +689,13 @@ struct StdArgs {
   uint32_t scripts_len;
   const hkv_input_job* jobs;
   int32_t forkid;
+  // the multisig scan the block kernel runs on its square-root wave
+  // (hkv_ms_scan_kernel's operands; null: the host launches the scan)
+  uint32_t* ms_desc;
+  uint64_t* ms_off;
+  unsigned long long* ms_ctr;
+  volatile unsigned long long* ms_host;
+  unsigned long long ms_seq;
 };
 
 // Pair-form pieces shared by the small-batch kernels (2c, 2d). Each chain
@@ -1184,6 +1191,13 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       if (ln < BLK_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
       blk_post(&bflag[BF_Y], seq);
       mark(STAMP_SQRT);
+      // STD: the multisig scan of the group's inputs (off every critical path)
+      if constexpr (STD) {
+        const uint32_t jx = base + ln;
+        if (sa.ms_desc != nullptr)
+          ms_scan_lane(sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, jx, ln < BLK_SIGS && jx < n,
+                       sa.forkid, sa.ms_desc, sa.ms_off, sa.ms_ctr, shabuf);
+      }
     } else {
       // ---- chain waves: lanes 0-31 k1, 32-63 k2 (two lanes per chain) ----
       const int half = (int)(ln >> 5);
@@ -1294,6 +1308,12 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       }
     }
     __syncthreads();  // the group's LDS (tables, exchanges, flags' data) is read before the next group's writes
+  }
+  if constexpr (STD) {  // the last workgroup publishes the batch's multisig record count
+    if (wv == 3 && sa.ms_desc != nullptr) {
+      __threadfence();
+      if (ln == 0) ms_scan_done(sa.ms_ctr, sa.ms_host, sa.ms_seq, gridDim.x);
+    }
   }
 }
 
@@ -2040,6 +2060,7 @@ hipError_t launch_prologue(const void* recs, uint32_t n, uint32_t n_pad, uint32_
 // workgroup); no separate prologue. mid: full-grid batches of at most 2
 // waves per SIMD, the paired-form instance at a 2-wave register allocation
 static inline bool block_batch(uint32_t n_pad, uint32_t n_cu) { return n_pad <= (uint32_t)BLK_SIGS * n_cu; }
+bool std_split_scans(uint32_t n_pad, uint32_t n_cu) { return block_batch(n_pad, n_cu); }
 hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* qs,
                          uint32_t grid, uint32_t* bits, uint32_t n_words, bool split, bool mid,
                          unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, uint32_t n_cu,
@@ -2050,7 +2071,7 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                        bits, n_words, aux, rw, mode, clk, StdArgs{});
   else if (split)
     hipLaunchKernelGGL(hkv_pair_split_kernel<false>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, aux, rw, mode, clk, StdArgs{});
+                       gtab, qs, bits, n_words, aux, rw, mode, clk, StdArgs{});  // (record batches: no std operands)
   else if (mid)
     hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
   else
@@ -2064,8 +2085,15 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
-                                   uint32_t n_cu, hipStream_t st) {
-  const StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid};
+                                   uint32_t n_cu, const MsScan* ms, hipStream_t st) {
+  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr, nullptr, 0ull};
+  if (ms != nullptr && block_batch(n_pad, n_cu)) {
+    sa.ms_desc = ms->desc;
+    sa.ms_off = ms->off;
+    sa.ms_ctr = reinterpret_cast<unsigned long long*>(ms->counters);
+    sa.ms_host = reinterpret_cast<volatile unsigned long long*>(ms->host_total);
+    sa.ms_seq = (unsigned long long)ms->seq;
+  }
   uint32_t* rw = reinterpret_cast<uint32_t*>(recs);
   if (block_batch(n_pad, n_cu))
     hipLaunchKernelGGL(hkv_block_kernel<true>, dim3(n_pad / BLK_SIGS), dim3(BLK_TPB), 0, st, im, n, n_pad, gtab, qs,

@@ -171,184 +171,8 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   std_write_record(r32, x, live, d);
 }
 
-// ---------------------------------------------------------------------------
-// 4. multisig inputs (bare and P2SH): candidate (signature, key) records
-// ---------------------------------------------------------------------------
-// haskoin-core verifyStdInput's PayMulSig branch [dep; oracle/sighash_oracle.py
-// std_multisig]: countMulSig walks the keys in order against the current
-// signature; a match consumes both, a miss only the key, an empty signature
-// (OP_0) one of each; the input verifies iff the count equals m and every
-// key of the script is a point (importPubKey). Which comparisons the walk
-// makes depends on earlier verdicts, so the batch checks every pair it could
-// make (signature j < min(#sigs, n) against keys j..n-1) and
-// hkv_ms_resolve_kernel replays the walk over the verdict bits.
-//   hkv_ms_scan_kernel    per input: template + scriptSig decode (+ the P2SH
-//                         redeem HASH160), desc words and candidate counts
-//   (exclusive scan of the counts -> record offsets)
-//   hkv_ms_emit_kernel    per input: sighash of each signature, candidate and
-//                         key-check records
-//   hkv_ms_resolve_kernel per input: the countMulSig walk -> verdict bit
-// Keys must be direct pushes (21 / 41) with PubKeyI prefixes, the limit the
-// P2PK template shares, so haskoin's canonical re-encoding (encodeOutput) of
-// the script equals its bytes.
-constexpr uint32_t MS_OK = 1u << 31, MS_P2SH = 1u << 30;
-
-// OP_m <keys> OP_n OP_CHECKMULTISIG, 1 <= m <= n <= 16
-HKV_DEV bool ms_template(const uint8_t* sc, uint32_t L, uint32_t& m, uint32_t& n) {
-  if (L < 3 || sc[L - 1] != 0xAEu) return false;
-  m = (uint32_t)sc[0] - 0x50u;
-  n = (uint32_t)sc[L - 2] - 0x50u;
-  if (m < 1u || m > 16u || n < 1u || n > 16u || m > n) return false;
-  uint32_t off = 1, k = 0;
-  while (off < L - 2 && k < 17u) {
-    const uint32_t op = sc[off];
-    if (op != 0x21u && op != 0x41u) return false;
-    if (off + 1 + op > L - 2) return false;
-    const uint32_t pre = sc[off + 1];
-    if (op == 0x21u ? (pre != 2u && pre != 3u) : (pre != 4u)) return false;
-    off += 1 + op;
-    ++k;
-  }
-  return off == L - 2 && k == n;
-}
-// key k of a validated template
-HKV_DEV const uint8_t* ms_key(const uint8_t* sc, uint32_t k, uint32_t& len) {
-  uint32_t off = 1;
-  for (uint32_t q = 0; q < k; ++q) off += 1 + sc[off];
-  len = sc[off];
-  return sc + off + 1;
-}
-// skip one script op (haskoin's Script parse: a push must fit)
-HKV_DEV bool skip_op(const uint8_t* p, uint32_t& off, uint32_t end) {
-  const uint32_t op = p[off];
-  if (op == 0u || op > 0x4Eu) {
-    ++off;
-    return true;
-  }
-  uint32_t d_off, d_len;
-  return read_push(p, off, end, d_off, d_len);
-}
-
-struct MsIn {
-  const uint8_t* code;  // scriptCode: the prevout, redeem or witness script
-  uint32_t code_len;
-  // the signature items: scriptSig form — the byte range after the OP_0
-  // dummy (and before a P2SH redeem push); witness form — it_off is the
-  // length varint of the item after the empty dummy, n_items of them
-  uint32_t it_off, it_end, n_items;
-  uint32_t m, n, s_eff, mask, n_cand;
-  bool p2sh, wit;            // HASH160(rd) == the P2SH hash; witness form (SHA-256 check, BIP143)
-  const uint8_t* rd;         // P2SH: the pushed redeem script (a multisig script, or 00 20 <h32>)
-  uint32_t rd_len;
-  const uint8_t* wprog;      // witness form: the 32-byte program
-};
-
-// next item: d_len == 0 means TxSignatureEmpty; false = not a push (decode fails)
-HKV_DEV bool ms_item(const uint8_t* txs, const MsIn& r, uint32_t& off, uint32_t& d_off, uint32_t& d_len) {
-  if (r.wit) {
-    d_len = get_varint(txs, off);
-    d_off = off;
-    off += d_len;
-    return true;
-  }
-  if (txs[off] == 0u) {
-    ++off;
-    d_len = 0;
-    return true;
-  }
-  return read_push(txs, off, r.it_end, d_off, d_len);
-}
-
-// decode a multisig input except the hash checks (P2SH HASH160, P2WSH SHA-256)
-HKV_DEV bool ms_parse(MsIn& r, const uint8_t* txs, const uint32_t* row, uint32_t input, const uint8_t* spk,
-                      uint32_t L, int32_t forkid) {
-  r.p2sh = L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u;
-  r.wit = false;
-  r.rd = txs;
-  r.rd_len = 0;
-  r.wprog = spk;
-  uint32_t in_off, ss_off, ss_len, seq_off;
-  walk_input(txs, row[TXT_INS], input, in_off, ss_off, ss_len, seq_off);
-  const uint32_t end = ss_off + ss_len;
-  if (L == 34u && spk[0] == 0u && spk[1] == 0x20u) {  // P2WSH: empty scriptSig
-    if (ss_len != 0) return false;
-    r.wit = true;
-    r.wprog = spk + 2;
-  } else if (r.p2sh && ss_len > 0 && txs[ss_off] != 0u) {  // P2SH-P2WSH: exactly one push of 00 20 <h32>
-    uint32_t c = ss_off, d_off = 0, d_len = 0;
-    if (!read_push(txs, c, end, d_off, d_len) || c != end || d_len != 34u || txs[d_off] != 0u ||
-        txs[d_off + 1] != 0x20u)
-      return false;
-    r.wit = true;
-    r.rd = txs + d_off;
-    r.rd_len = 34;
-    r.wprog = r.rd + 2;
-  }
-  if (r.wit) {  // witness = [empty dummy] ++ items ++ [witness script]
-    if (!(row[TXT_FLAGS] & TXF_WITNESS)) return false;
-    uint32_t w = walk_witness(txs, row[TXT_OUTS_END], input);
-    const uint32_t cnt = get_varint(txs, w);
-    if (cnt < 2u || get_varint(txs, w) != 0u) return false;
-    r.it_off = w;
-    r.n_items = cnt - 2u;
-    for (uint32_t k = 0; k < r.n_items; ++k) w += get_varint(txs, w);
-    r.code_len = get_varint(txs, w);
-    r.code = txs + w;
-    r.it_end = w;
-  } else {
-    if (ss_len == 0 || txs[ss_off] != 0u) return false;  // haskoin matchMulSig: OP_0 first
-    r.it_off = ss_off + 1;
-    if (r.p2sh) {
-      uint32_t off = ss_off + 1, last = 0, n_ops = 0;
-      while (off < end) {
-        last = off;
-        if (!skip_op(txs, off, end)) return false;
-        ++n_ops;
-      }
-      if (n_ops == 0) return false;
-      uint32_t c = last, d_off = 0, d_len = 0;
-      if (!read_push(txs, c, end, d_off, d_len)) return false;  // the redeem script: OP_PUSHDATA
-      r.code = r.rd = txs + d_off;
-      r.code_len = r.rd_len = d_len;
-      r.it_end = last;
-    } else {
-      r.code = spk;
-      r.code_len = L;
-      r.it_end = end;
-    }
-    r.n_items = 0xFFFFFFFFu;  // until it_end
-  }
-  if (!ms_template(r.code, r.code_len, r.m, r.n)) return false;
-  uint32_t j = 0, mask = 0, cand = 0, off = r.it_off;
-  while (r.wit ? j < r.n_items : off < r.it_end) {
-    uint32_t d_off = 0, d_len = 0;
-    if (!ms_item(txs, r, off, d_off, d_len)) return false;  // any other op fails the decode
-    if (d_len) {
-      uint32_t rr[8], ss[8], sh;
-      if (!decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh)) return false;
-      if (j < r.n) {
-        mask |= 1u << j;
-        cand += r.n - j;
-      }
-    }
-    ++j;
-  }
-  r.s_eff = j < r.n ? j : r.n;
-  r.mask = mask;
-  r.n_cand = cand;
-  return true;
-}
-
-// job -> (row, prevout script); false for a bad reference / unparsed tx
-HKV_DEV bool ms_job(const hkv_input_job& jb, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                    uint32_t scripts_len, const uint32_t*& row, const uint8_t*& spk) {
-  if (!(jb.tx < n_tx && jb.script_off <= scripts_len && scripts_len - jb.script_off >= jb.script_len)) return false;
-  row = txt + (size_t)jb.tx * TXT_WORDS;
-  if (!((row[TXT_FLAGS] & TXF_OK) && jb.input < row[TXT_NIN])) return false;
-  spk = scripts + jb.script_off;
-  return true;
-}
-
+// 4. multisig inputs: the scan (hkv_sighash_dev.h ms_scan_lane), candidate
+//    records, the countMulSig walk
 __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
                                                          const uint32_t* __restrict__ txt,
                                                          const uint8_t* __restrict__ scripts, uint32_t scripts_len,
@@ -358,73 +182,12 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
                                                          unsigned long long* __restrict__ counters,
                                                          volatile unsigned long long* __restrict__ host_total,
                                                          unsigned long long seq) {
-  unsigned long long* total = counters;                                  // candidates | keys << 32
-  unsigned int* done = reinterpret_cast<unsigned int*>(counters + 1);    // finished workgroups
   __shared__ uint32_t buf[16 * WG];
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
-  MsIn r;
-  r.p2sh = r.wit = false;
-  r.code = r.rd = r.wprog = scripts;
-  r.code_len = r.rd_len = 0;
-  bool ok = false;
-  const uint8_t* spk = scripts;
-  if (jx < n) {
-    const hkv_input_job jb = jobs[jx];
-    const uint32_t* row = txt;
-    ok = ms_job(jb, n_tx, txt, scripts, scripts_len, row, spk);
-    if (ok) {
-      const uint32_t L = jb.script_len;
-      const bool p2sh = L == 23u && spk[0] == 0xA9u && spk[1] == 0x14u && spk[22] == 0x87u;
-      const bool p2wsh = L == 34u && spk[0] == 0u && spk[1] == 0x20u;
-      const bool bare = L >= 3u && spk[L - 1] == 0xAEu;
-      ok = (p2sh || p2wsh || bare) && ms_parse(r, txs, row, jb.input, spk, L, forkid);
-    }
-  }
-  Gen g;
-  uint32_t h[8];
-  // P2SH: HASH160(redeem script) == the script hash
-  const bool need = ok && r.p2sh;
-  if (__any(need)) {
-    gen_clear(g);
-    g.code = r.rd;
-    g.code_len = r.rd_len;
-    g.phase = PH_RANGE;
-    sha256_stream(h, g, need, buf);
-    uint32_t rip[5];
-    ripemd160_of_digest(rip, h);
-    if (need) ok = ok && eq_h160(spk + 2, rip);
-  }
-  // P2WSH (native or nested): SHA-256(witness script) == the program
-  const bool need_ws = ok && r.wit;
-  if (__any(need_ws)) {
-    gen_clear(g);
-    g.code = r.code;
-    g.code_len = r.code_len;
-    g.phase = PH_RANGE;
-    sha256_stream(h, g, need_ws, buf);
-    if (need_ws) ok = ok && eq_sha256(r.wprog, h);
-  }
-  if (jx < n) {
-    desc[2 * (size_t)jx] = ok ? (MS_OK | (r.p2sh ? MS_P2SH : 0u) | r.m | (r.n << 8) | (r.s_eff << 16)) : 0u;
-    desc[2 * (size_t)jx + 1] = ok ? r.mask : 0u;
-    // record ranges: candidates in the low 32 bits, key checks in the high 32
-    // (their sums stay below 2^32); placement order is irrelevant to verdicts
-    off[jx] = ok ? (uint64_t)atomicAdd(total, (unsigned long long)r.n_cand | ((unsigned long long)r.n << 32)) : 0ull;
-  }
-  // The last workgroup to finish publishes the sum to the caller's pinned
-  // host word and re-arms both device counters, so the stream carries no
-  // memset and no D2H copy (the host waits on an event after this kernel).
+  ms_scan_lane(txs, n_tx, txt, scripts, scripts_len, jobs, jx, jx < n, forkid, desc, off, counters, buf);
   __threadfence();
   __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
-    __threadfence();
-    const unsigned long long t = atomicExch(total, 0ull);
-    atomicExch(done, 0u);
-    host_total[0] = t;
-    __threadfence_system();
-    host_total[1] = seq;  // the host polls this word
-    __threadfence_system();
-  }
+  if (threadIdx.x == 0) ms_scan_done(counters, host_total, seq, gridDim.x);
 }
 
 // record: msg32 (digest byte order words) | r | s (limbs, written big-endian) |
