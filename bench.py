@@ -216,13 +216,16 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
     return res, got
 
 
-PHASES = ("start", "k1_table", "barrier_P", "k1_chain", "barrier_A", "join", "sig_parse", "u1G", "key_sqrt",
-          "k2_table", "k2_chain")
+# phase slots of the block kernel (hkv_kernels.hip 2d): wave 0 (low windows),
+# wave 1 (2^(4 K1) Q' / 2^(4 K2) Q' and the high windows), wave 2 (signature),
+# wave 3 (key sqrt, then the middle windows)
+PHASES = ("start", "lo_table", "digits", "lo_chain", "a_y0", "verdict", "sig_parse", "u1G", "key_sqrt",
+          "hi_table", "hi_chain", "mid_chain")
 
 
 def split_phases(v, torch, run) -> dict:
-    """Phase boundaries of workgroup 0 of the small-batch (split) kernel in
-    one extra profiled call (hkv_profile_phases: constant-rate clock stamps,
+    """Phase boundaries of workgroup 0 of the small-batch kernel in one extra
+    profiled call (hkv_profile_phases: constant-rate clock stamps,
     microseconds after the kernel's start)."""
     v.lib.hkv_profile_enable(v.ctx, 1)
     run()

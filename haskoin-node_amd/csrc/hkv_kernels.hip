@@ -1107,30 +1107,38 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
 // 2d. Block kernel (a block: at most BLK_SIGS signatures per CU). In the
 //     pair kernel one signature's chain is the latency: 128 doublings and 33
 //     additions of one pair of lanes, started only once the signature is
-//     parsed (the digits). Here the radix-16 windows are split at BLK_K:
-//       wave 0: windows 0..BLK_K-1 against the table of Q' (lanes 0-31 k1,
-//               lanes 32-63 k2), then S_lo = their sum and T = A + S_lo on E;
-//       wave 1: first Q4 = 2^(4 BLK_K) Q' by 4 BLK_K pair doublings from
-//               t = 0 (no digits needed), then the table of Q4 and windows
-//               BLK_K..NWIN-1 against it (lanes 0-31 k1, 32-63 k2), then
-//               S_hi, R = T + S_hi on E, the x compare and the verdicts;
-//       wave 2: the signature (lanes 0-15), then u1 * G (STD: the hashes);
-//       wave 3: the key's y0 = sqrt(w) (lanes 0-15).
-//     The doublings on wave 1's path stay 128, but only NWIN - BLK_K of the
-//     additions lie on it and the signature parse is hidden behind Q4.
+//     parsed (the digits). Here each chain's radix-16 windows are cut in
+//     three segments, each run against the table of its own base point:
+//       wave 0: windows 0..K1-1 against the table of Q' (lanes 0-31 k1,
+//               lanes 32-63 k2); then S_lo = their sum and T = A + S_lo on E;
+//       wave 1: Q1 = 2^(4 K1) Q' and Q2 = 2^(4 K2) Q' by doublings from t = 0
+//               (four lanes per signature, quad_double; Q1 is handed to wave
+//               3 on the way), then the table of Q2 and windows K2..NWIN-1;
+//               then S_hi, R = U + S_hi on E, the x compare, the verdicts;
+//       wave 3: the key's y0 = sqrt(w) (lanes 0-15), then the table of Q1 and
+//               windows K1..K2-1; then S_mid and U = T + S_mid on E;
+//       wave 2: the signature (lanes 0-15), then u1 * G (STD: the hashes,
+//               then the multisig scan of the group's inputs).
+//     The doublings on wave 1's path stay 128 (the floor for a 128-bit
+//     scalar), but only NWIN - K2 of the additions and none of the waits for
+//     the signature lie on it; waves 0 and 3 work beside it.
 //     16 signatures per workgroup of 4 waves (one per SIMD): a 4,000-input
 //     block fills 250 CUs. The hand-offs are LDS flags (release / acquire at
 //     workgroup scope) instead of workgroup barriers, so no wave waits at a
 //     barrier for a phase it does not need.
 // ---------------------------------------------------------------------------
-#ifndef HKV_BLK_K
-#define HKV_BLK_K 23
+#ifndef HKV_BLK_K1
+#define HKV_BLK_K1 18
 #endif
-constexpr int BLK_K = HKV_BLK_K;
-static_assert(BLK_K >= 2 && BLK_K <= NWIN - 2, "both chains take windows");
+#ifndef HKV_BLK_K2
+#define HKV_BLK_K2 28
+#endif
+constexpr int BLK_K1 = HKV_BLK_K1, BLK_K2 = HKV_BLK_K2;
+static_assert(BLK_K1 >= 2 && BLK_K1 < BLK_K2 && BLK_K2 <= NWIN - 1, "three non-empty segments");
 constexpr int BLK_SIGS = 16;
 constexpr int BLK_TPB = 256;
-enum : int { BF_SIG = 0, BF_A = 1, BF_Y = 2, BF_T = 3, BF_COUNT = 4 };
+enum : int { BF_SIG = 0, BF_A = 1, BF_Y = 2, BF_T = 3, BF_Q = 4, BF_U = 5, BF_COUNT = 6 };
+constexpr int STAMP_CHAIN_MID = STAMP_COUNT;  // the twelfth phase slot (hkv_profile_phases reads 12)
 // publish: every prior write of the wave (LDS and global) before the flag
 HKV_DEV void blk_post(uint32_t* f, uint32_t seq) {
   __threadfence_block();
@@ -1145,6 +1153,35 @@ HKV_DEV void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// A chain wave's two halves (lanes 0-31 k1, 32-63 k2) summed on the k1
+// lanes: S (valid on the even lanes of 0-31) on the wave's curve
+HKV_DEV void halves_sum(uint32_t* xk, uint32_t c, int half, uint32_t odd, const fe& P, const fe& Z, bool inf, gej& S,
+                        bool& sinf) {
+  if (half == 1) pair_publish(xk, BLK_SIGS, c, P, Z, inf, odd);
+  fe Y, Zx;
+  fe_xch(Y, P);   // even lane: Y of the pair
+  fe_xch(Zx, Z);  // even lane: Z of the pair
+  wave_lds_sync();
+  S.x = P;
+  S.y = Y;
+  S.z = Zx;
+  sinf = inf;
+  if (half == 0) {
+    gej b;
+    bool binf;
+    xch_read(xk, BLK_SIGS, c, b, binf);
+    gej_add_var(S, sinf, b, binf);
+  }
+}
+// acc (on E) += phi^-1 of a segment's sum S: S is Jacobian on E_w at the
+// isomorphic scale zs (its table's Zg times its base point's Z), so on E it
+// is (X, Y, Z zs y0)
+HKV_DEV void add_segment(gej& acc, bool& ainf, gej S, bool sinf, const fe& zs, const fe& y0) {
+  fe zt;
+  fe_mul(zt, S.z, zs);
+  fe_mul(S.z, zt, y0);
+  gej_add_var(acc, ainf, S, sinf);
+}
 
 template <bool STD>
 __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
@@ -1154,15 +1191,16 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
                                                                uint32_t* __restrict__ aux,
                                                                uint32_t* __restrict__ recs, uint32_t mode,
                                                                unsigned long long* __restrict__ clk, StdArgs sa) {
-  __shared__ QLane qlds[2];
-  __shared__ uint32_t xch[3][25 * BLK_SIGS];  // k2 -> k1 of wave 0, of wave 1; T wave 0 -> wave 1
+  __shared__ QLane qlds[3];                     // the Q' (wave 0), Q2 (wave 1) and Q1 (wave 3) tables
+  __shared__ uint32_t xch[5][25 * BLK_SIGS];    // k2 -> k1 of waves 0, 1, 3; T (0 -> 3); U (3 -> 1)
+  __shared__ uint32_t qpub[3][8][BLK_SIGS];     // Q1 = (X, Y, Z), wave 1 -> wave 3
   __shared__ uint32_t shabuf[STD ? 16 * WG : 1];
   __shared__ uint32_t bflag[BF_COUNT];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
-  const uint32_t n_lanes = gridDim.x * 128u;
-  const uint32_t qlane = blockIdx.x * 128u + (threadIdx.x & 127u);
+  const uint32_t n_lanes = gridDim.x * 192u;  // chain lanes of the launch (qs scratch): waves 0, 1, 3
+  const uint32_t qlane = blockIdx.x * 192u + (uint32_t)(wv == 3 ? 2 : wv) * 64u + ln;
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
     if (stamp) clk[4 + slot] = wall_clock64();
@@ -1187,130 +1225,139 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       sig_wave_gsum<STD>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
       blk_post(&bflag[BF_A], seq);
       mark(STAMP_GSUM);
-    } else if (wv == 3) {
+      // STD: the multisig scan of the group's inputs (off every critical path)
+      if constexpr (STD) {
+        if (sa.ms_desc != nullptr)
+          ms_scan_lane(sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, on && i < n, sa.forkid,
+                       sa.ms_desc, sa.ms_off, sa.ms_ctr, shabuf);
+      }
+      __syncthreads();  // the group's LDS is read before the next group's writes
+      continue;
+    }
+    // ---- chain waves 0, 1, 3: lanes 0-31 k1, 32-63 k2 (two lanes per chain) ----
+    const int half = (int)(ln >> 5);
+    const uint32_t c = (ln & 31u) >> 1;
+    const uint32_t i = base + c;
+    const int slot = wv == 3 ? 2 : wv;            // table / exchange slot of the wave
+    fe Zg, zb, P, Z;                              // table scale, base point's Z
+    if (wv == 0) {
+      ge q;
+      key_point<STD>(i, n, recs, sa, q);
+      fe_sel(P, q.x, q.y, odd);
+      fe_set_u32(zb, 1);
+      pair_table(P, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
+      mark(STAMP_TABLE0);
+    } else if (wv == 1) {
+      // Q1, Q2 on four lanes per signature (lanes 4c'..4c'+3: X | Y | Z | .)
+      const uint32_t cq = ln >> 2, qd = ln & 3u;
+      const uint32_t m0 = qd == 0 ? ~0u : 0u, m1 = qd == 1 ? ~0u : 0u, m2 = qd == 2 ? ~0u : 0u;
+      ge q;
+      key_point<STD>(base + cq, n, recs, sa, q);
+      fe V;
+      fe_set_u32(V, 1);
+      fe_sel(V, V, q.y, m1);
+      fe_sel(V, V, q.x, m0);  // x | y | 1 | 1
+#pragma unroll 1
+      for (int d = 0; d < QW * BLK_K1; ++d) quad_double(V, m0, m1, m2);
+      if (qd < 3) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qpub[qd][k][cq] = V.v[k];
+      }
+      blk_post(&bflag[BF_Q], seq);
+#pragma unroll 1
+      for (int d = QW * BLK_K1; d < QW * BLK_K2; ++d) quad_double(V, m0, m1, m2);
+      // to the chains' pair layout: X2 | Y2 with Z2 on both lanes; (X2, Y2) is
+      // an affine point of the isomorphic curve of scale Z2
+      const int src_p = (int)(4 * c + (odd ? 1u : 0u)), src_z = (int)(4 * c + 2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        P.v[k] = (uint32_t)__shfl((int)V.v[k], src_p);
+        zb.v[k] = (uint32_t)__shfl((int)V.v[k], src_z);
+      }
+      pair_table(P, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
+      mark(STAMP_TABLE1);
+    } else {
       if (ln < BLK_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
       blk_post(&bflag[BF_Y], seq);
       mark(STAMP_SQRT);
-      // STD: the multisig scan of the group's inputs (off every critical path)
-      if constexpr (STD) {
-        const uint32_t jx = base + ln;
-        if (sa.ms_desc != nullptr)
-          ms_scan_lane(sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, jx, ln < BLK_SIGS && jx < n,
-                       sa.forkid, sa.ms_desc, sa.ms_off, sa.ms_ctr, shabuf);
-      }
-    } else {
-      // ---- chain waves: lanes 0-31 k1, 32-63 k2 (two lanes per chain) ----
-      const int half = (int)(ln >> 5);
-      const uint32_t c = (ln & 31u) >> 1;
-      const uint32_t i = base + c;
-      fe Zg, z4, P, Z;
-      if (wv == 0) {
-        ge q;
-        key_point<STD>(i, n, recs, sa, q);
-        fe_sel(P, q.x, q.y, odd);
-        fe_set_u32(z4, 1);
-        pair_table(P, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
-        mark(STAMP_TABLE0);
-      } else {
-        // Q4 = 2^(4 BLK_K) Q' on four lanes per signature (lanes 4c'..4c'+3,
-        // quad_double: S + 2M per doubling), then to the chains' pair layout:
-        // X4 | Y4 with Z4 on both lanes, (X4, Y4) an affine point of the
-        // isomorphic curve of scale Z4
-        const uint32_t cq = ln >> 2, qd = ln & 3u;
-        const uint32_t m0 = qd == 0 ? ~0u : 0u, m1 = qd == 1 ? ~0u : 0u, m2 = qd == 2 ? ~0u : 0u;
-        ge q;
-        key_point<STD>(base + cq, n, recs, sa, q);
-        fe V;
-        fe_set_u32(V, 1);
-        fe_sel(V, V, q.y, m1);
-        fe_sel(V, V, q.x, m0);  // x | y | 1 | 1
-#pragma unroll 1
-        for (int d = 0; d < QW * BLK_K; ++d) quad_double(V, m0, m1, m2);
-        const int src_p = (int)(4 * c + (odd ? 1u : 0u)), src_z = (int)(4 * c + 2);
+      blk_wait(&bflag[BF_Q], seq);  // Q1 from wave 1
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          P.v[k] = (uint32_t)__shfl((int)V.v[k], src_p);
-          z4.v[k] = (uint32_t)__shfl((int)V.v[k], src_z);
-        }
-        pair_table(P, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
-        mark(STAMP_TABLE1);
+      for (int k = 0; k < 8; ++k) {
+        P.v[k] = qpub[odd ? 1 : 0][k][c];
+        zb.v[k] = qpub[2][k][c];
       }
-      blk_wait(&bflag[BF_SIG], seq);  // the digits, r and flags are in im
-      if (wv == 0) mark(STAMP_P);
-      const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-      const bool valid = (i < n) && (flags & FLAG_VALID);
-      const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
-      bool inf;
-      if (wv == 0) pair_chain(P, Z, inf, qlds[0], im, n_pad, i, valid, negh, half, odd, ln, BLK_K - 1, 0);
-      else pair_chain(P, Z, inf, qlds[1], im, n_pad, i, valid, negh, half, odd, ln, NWIN - 1, BLK_K);
-      mark(wv == 0 ? STAMP_CHAIN0 : STAMP_CHAIN1);
-      // ---- k2's part to k1's lanes (same wave), S = k1 part + k2 part ----
-      uint32_t* xk = xch[wv];
-      if (half == 1) pair_publish(xk, BLK_SIGS, c, P, Z, inf, odd);
-      fe Y, Zx;
-      fe_xch(Y, P);   // even lane: Y of the pair
-      fe_xch(Zx, Z);  // even lane: Z of the pair
-      wave_lds_sync();
-      gej S;
-      S.x = P;
-      S.y = Y;
-      S.z = Zx;
-      bool sinf = inf;
+      pair_table(P, half, odd, qs, n_lanes, qlane, qlds[2], ln, Zg);
+    }
+    blk_wait(&bflag[BF_SIG], seq);  // the digits, r and flags are in im
+    if (wv == 0) mark(STAMP_P);
+    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+    const bool valid = (i < n) && (flags & FLAG_VALID);
+    const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
+    const int w_hi = wv == 0 ? BLK_K1 - 1 : (wv == 1 ? NWIN - 1 : BLK_K2 - 1);
+    const int w_lo = wv == 0 ? 0 : (wv == 1 ? BLK_K2 : BLK_K1);
+    bool inf;
+    pair_chain(P, Z, inf, qlds[slot], im, n_pad, i, valid, negh, half, odd, ln, w_hi, w_lo);
+    mark(wv == 0 ? STAMP_CHAIN0 : (wv == 1 ? STAMP_CHAIN1 : STAMP_CHAIN_MID));
+    gej S;
+    bool sinf;
+    halves_sum(xch[slot], c, half, odd, P, Z, inf, S, sinf);  // on E_w at scale Zg * zb
+    fe zs;
+    fe_mul(zs, Zg, zb);
+    if (wv == 0) {
+      // ---- T = A + phi^-1(S_lo) on E (A = u1 G, y0 the key's y) ----
+      blk_wait(&bflag[BF_A], seq);
+      blk_wait(&bflag[BF_Y], seq);
+      mark(STAMP_A);
       if (half == 0) {
-        gej b;
-        bool binf;
-        xch_read(xk, BLK_SIGS, c, b, binf);
-        gej_add_var(S, sinf, b, binf);  // on E_w at iso scale Zg * z4
+        gej A;
+        fe y0;
+        uint32_t r[8], af;
+        bool is_sq;
+        join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
+        bool tinf = (af & AUXF_AINF) != 0;
+        add_segment(A, tinf, S, sinf, zs, y0);
+        if (!odd) xch_write(xch[3], BLK_SIGS, c, A, tinf);
       }
-      if (wv == 0) {
-        // ---- T = A + phi^-1(S_lo) on E (A = u1 G, y0 the key's y) ----
-        blk_wait(&bflag[BF_A], seq);
-        blk_wait(&bflag[BF_Y], seq);
-        mark(STAMP_A);
-        if (half == 0) {
-          gej A;
-          fe y0;
-          uint32_t r[8], af;
-          bool is_sq;
-          join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
-          fe zt;
-          fe_mul(zt, S.z, Zg);
-          fe_mul(S.z, zt, y0);
-          bool tinf = (af & AUXF_AINF) != 0;
-          gej_add_var(A, tinf, S, sinf);
-          if (!odd) xch_write(xch[2], BLK_SIGS, c, A, tinf);
-        }
-        blk_post(&bflag[BF_T], seq);
-      } else {
-        // ---- R = T + phi^-1(S_hi) on E, the x compare, the verdicts ----
-        blk_wait(&bflag[BF_T], seq);
-        bool accept = false;
-        if (half == 0) {
-          gej A, T;
-          fe y0;
-          uint32_t r[8], af;
-          bool is_sq, tinf;
-          join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
-          xch_read(xch[2], BLK_SIGS, c, T, tinf);
-          fe zt;
-          fe_mul(zt, S.z, Zg);
-          fe_mul(zt, zt, z4);
-          fe_mul(S.z, zt, y0);
-          gej_add_var(T, tinf, S, sinf);
-          accept = valid && is_sq && !tinf && x_matches_r(T.x, T.z, r) && (!STD || (af & AUXF_STDOK));
-        }
-        const uint64_t ball = __ballot(accept && !odd);
-        mark(STAMP_JOIN);
-        if (ln == 0) {
-          const uint32_t wi = base / 32;
-          if (wi < n_words) reinterpret_cast<uint16_t*>(bits)[base / BLK_SIGS] = (uint16_t)(even_bits(ball) & 0xFFFFu);
-        }
+      blk_post(&bflag[BF_T], seq);
+    } else if (wv == 3) {
+      // ---- U = T + phi^-1(S_mid) on E ----
+      blk_wait(&bflag[BF_T], seq);
+      if (half == 0) {
+        gej T;
+        bool tinf;
+        fe y0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+        xch_read(xch[3], BLK_SIGS, c, T, tinf);
+        add_segment(T, tinf, S, sinf, zs, y0);
+        if (!odd) xch_write(xch[4], BLK_SIGS, c, T, tinf);
+      }
+      blk_post(&bflag[BF_U], seq);
+    } else {
+      // ---- R = U + phi^-1(S_hi) on E, the x compare, the verdicts ----
+      blk_wait(&bflag[BF_U], seq);
+      bool accept = false;
+      if (half == 0) {
+        gej A, R;
+        fe y0;
+        uint32_t r[8], af;
+        bool is_sq, rinf;
+        join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
+        xch_read(xch[4], BLK_SIGS, c, R, rinf);
+        add_segment(R, rinf, S, sinf, zs, y0);
+        accept = valid && is_sq && !rinf && x_matches_r(R.x, R.z, r) && (!STD || (af & AUXF_STDOK));
+      }
+      const uint64_t ball = __ballot(accept && !odd);
+      mark(STAMP_JOIN);
+      if (ln == 0) {
+        const uint32_t wi = base / 32;
+        if (wi < n_words) reinterpret_cast<uint16_t*>(bits)[base / BLK_SIGS] = (uint16_t)(even_bits(ball) & 0xFFFFu);
       }
     }
     __syncthreads();  // the group's LDS (tables, exchanges, flags' data) is read before the next group's writes
   }
   if constexpr (STD) {  // the last workgroup publishes the batch's multisig record count
-    if (wv == 3 && sa.ms_desc != nullptr) {
+    if (wv == 2 && sa.ms_desc != nullptr) {
       __threadfence();
       if (ln == 0) ms_scan_done(sa.ms_ctr, sa.ms_host, sa.ms_seq, gridDim.x);
     }
