@@ -906,7 +906,10 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
 // The signature wave, second half (whole wave: the STD hashes are
 // block-synchronous): STD — the script checks, the sighash and the input's
 // verify record; then u1 = m / s and A = u1 G into aux.
-template <bool STD>
+// SPREAD: the signature inputs are lanes 0..SPREAD-1 and the wave's other
+// lanes compute the three BIP143 per-tx hashes side by side (the block
+// kernel, SPREAD = 16); 0: each input's lane computes them in turn.
+template <bool STD, int SPREAD = 0>
 HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im,
                            const uint32_t* __restrict__ gtab, uint32_t* __restrict__ aux, uint32_t* __restrict__ recs,
                            const StdArgs& sa, uint32_t* shabuf, StdIn& x, sc m, const sc& sinv, bool use,
@@ -919,7 +922,9 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
     // (r32 is scratch until the record is written: words 0-7 for a BIP143
     // SINGLE hashOutputs, 8-31 for the tx's BIP143 hashes, which the fused
     // launch computes per input instead of an index-kernel pass)
-    const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8);
+    if constexpr (SPREAD > 0)  // every input that may sign with the BIP143 form
+      bip143_tx_hashes_spread(sa.txs, x.row, x.ok && (x.segwit || sa.forkid >= 0), r32 + 8, shabuf, SPREAD);
+    const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8, SPREAD > 0);
     if (on) {
       if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
       uint32_t w[8];
@@ -1222,7 +1227,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags);
       blk_post(&bflag[BF_SIG], seq);
       mark(STAMP_SIG);
-      sig_wave_gsum<STD>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
+      sig_wave_gsum<STD, BLK_SIGS>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
       blk_post(&bflag[BF_A], seq);
       mark(STAMP_GSUM);
       // STD: the multisig scan of the group's inputs (off every critical path)

@@ -971,6 +971,42 @@ HKV_DEV void bip143_tx_hashes(const uint8_t* __restrict__ txs, const uint32_t* r
   }
 }
 
+// The same three hashes for the G inputs on lanes 0..G-1 of a wave whose
+// other lanes are idle (the block kernel's signature wave, G = 16): lane
+// w G + c computes hash w of input c's tx, so the three streams run as one
+// block-synchronous stream; the digests go to input c's h3 scratch. Call
+// from wave-uniform control flow with every lane of the wave.
+HKV_DEV void bip143_tx_hashes_spread(const uint8_t* __restrict__ txs, const uint32_t* row, bool need, uint32_t* h3,
+                                     uint32_t* buf, uint32_t G) {
+  const uint32_t L = threadIdx.x & 63u, c = L % G, which = L / G;
+  const uint64_t rp = reinterpret_cast<uint64_t>(row), hp = reinterpret_cast<uint64_t>(h3);
+  const uint64_t rc = (uint64_t)(uint32_t)__shfl((int)(uint32_t)rp, (int)c) |
+                      ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rp >> 32), (int)c) << 32);
+  const uint64_t hc = (uint64_t)(uint32_t)__shfl((int)(uint32_t)hp, (int)c) |
+                      ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(hp >> 32), (int)c) << 32);
+  const bool go = __shfl(need ? 1 : 0, (int)c) != 0 && which < 3u;
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(rc);
+  Gen g;
+  uint32_t h[8], d[8];
+  gen_clear(g);
+  g.T = txs;
+  if (go) {
+    if (which == 2) {  // hashOutputs (each output re-serialised canonically)
+      g.ooff = rw[TXT_OUTS_FIRST]; g.ocnt = rw[TXT_NOUT]; g.ret = PH_DONE; g.phase = PH_O_VAL;
+    } else {
+      g.nin = rw[TXT_NIN]; g.ioff = rw[TXT_INS]; g.j = 0; g.phase = which == 0 ? PH_P_IN : PH_S_IN;
+    }
+  }
+  sha256_stream(h, g, go, buf);
+  sha256d_finish(d, h);
+  if (go) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(hc);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[8 * which + k] = d[k];
+  }
+  __threadfence_block();  // the digests before the owning lanes read them
+}
+
 // Part B: the HASH160 / SHA-256 script checks and the sighash (updates x.ok).
 // Call from wave-uniform control flow (block-synchronous SHA-256 streams
 // through buf[16 * WG]). single_ho: 8 scratch words of the lane (BIP143
@@ -980,7 +1016,7 @@ HKV_DEV void bip143_tx_hashes(const uint8_t* __restrict__ txs, const uint32_t* r
 // the sighash; false with x.ok means the legacy SINGLE bug (the message is
 // the integer 1).
 HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid, uint32_t* single_ho, uint32_t* buf,
-                      uint32_t d[8], uint32_t* h3 = nullptr) {
+                      uint32_t d[8], uint32_t* h3 = nullptr, bool h3_ready = false) {
   bool ok = x.ok;
   const uint32_t* row = x.row;
   const uint8_t* spk = x.spk;
@@ -1041,7 +1077,7 @@ HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid,
     }
   }
   const bool live = ok && !c.one;
-  if (h3 != nullptr) {
+  if (h3 != nullptr && !h3_ready) {
     const bool need_tx = live && c.forkid_form;
     if (__any(need_tx)) bip143_tx_hashes(txs, row, need_tx, h3, buf);
   }
