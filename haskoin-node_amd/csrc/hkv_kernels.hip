@@ -707,14 +707,19 @@ typedef uint32_t QLane[QTAB_ENTRIES][8][64];
 // j * q, j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg, in pair
 // form: Q = x | y is affine on its own curve (the a = 0 formulas never use
 // b). Forward: 2Q, Q' = phi_Z2(Q), P_{j+1} = P_j + Q' (pair additions; each
-// lane streams its coordinate and the z-ratio H_{j+1} to the lane's qs
-// scratch); backward: rho_j = prod_{k>j} H_k, entry j = (x rho^2, y rho^3)
-// (beta * x on the half-1 even lanes) straight into the LDS table — four
-// product levels per entry (rho H, rho^2, [x beta | rho^3], [. t | y rho^3])
-// instead of six one-lane products. Returns Zg on both lanes.
-HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, uint32_t* __restrict__ qs, uint32_t n_lanes,
-                        uint32_t qlane, QLane& ql, uint32_t ln, fe& Zg) {
-  const uint32_t plane = qlane & ~1u;  // the pair's even lane (its H slots)
+// lane keeps its raw coordinate in its LDS table slot, the pair's even lane
+// the z-ratio H_{j+1} in hl); backward: rho_j = prod_{k>j} H_k, entry j =
+// (x rho^2, y rho^3) (beta * x on the half-1 even lanes) rescaled in place —
+// four product levels per entry (rho H, rho^2, [x beta | rho^3],
+// [. rho^2 | y rho^3]) instead of six one-lane products, and no global
+// scratch round trip on the dependent loads. Returns Zg on both lanes.
+typedef uint32_t HLane[QTAB_ENTRIES - 1][8][32];
+HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, QLane& ql, HLane& hl, uint32_t ln, fe& Zg) {
+  const uint32_t pc = (ln >> 1) & 31u;  // the pair's H slot
+  auto put = [&](int j, const fe& v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ql[j][k][ln] = v.v[k];
+  };
   fe P = Q, Z, O1, O2, zz, zs, R, Qp;
   fe_set_u32(Z, 1);
   pair_double(P, Z, odd);     // 2Q = X2 | Y2, Z2 on the odd lane
@@ -724,17 +729,19 @@ HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, uint32_t* __restric
   fe_mul(R, O1, zs);          // x Z2^2         | Z2^3
   fe_mul(O2, Q, R);           //                | y Z2^3
   fe_sel(Qp, R, O2, odd);     // Q' = phi_Z2(Q): x Z2^2 | y Z2^3
-  qtab_store(qs, n_lanes, qlane, 0, 0, Qp);
-  qtab_store(qs, n_lanes, qlane, 1, 0, P);
+  put(0, Qp);
+  put(1, P);
   fe_set_u32(Z, 1);           // P_2 = (X2, Y2, 1) on the curve of scale Z2
 #pragma unroll 1
   for (int j = 2; j < QTAB_ENTRIES; ++j) {
     fe H;
     pair_add_affine(P, Z, Qp, odd, H);
-    qtab_store(qs, n_lanes, qlane, j, 0, P);
-    if (!odd) qtab_store(qs, n_lanes, qlane, j - 1, 2, H);  // H_{j+1}
+    put(j, P);
+    if (!odd) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) hl[j - 1][k][pc] = H.v[k];  // H_{j+1}
+    }
   }
-  __threadfence_block();      // the even lanes' H stores before the odd lanes' loads
   fe zc;
   fe_bc1(zc, Z);
   fe_mul(Zg, zz, zc);         // total scale: phi_Z2 then phi_Zc
@@ -747,8 +754,7 @@ HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, uint32_t* __restric
   {
     fe bx;
     fe_mul(bx, P, bsel);      // beta x | y (x 1)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ql[QTAB_ENTRIES - 1][k][ln] = bx.v[k];
+    put(QTAB_ENTRIES - 1, bx);
   }
   fe rho;
   fe_set_u32(rho, 1);
@@ -756,10 +762,12 @@ HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, uint32_t* __restric
   for (int j = QTAB_ENTRIES - 2; j >= 0; --j) {
     fe c, t, h;
     if (j >= 1) {
-      qtab_load(qs, n_lanes, plane, j, 2, h);  // H_{j+1}
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h.v[k] = hl[j][k][pc];  // H_{j+1}
       fe_mul(rho, rho, h);
     }
-    qtab_load(qs, n_lanes, qlane, j, 0, c);    // x | y of entry j
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c.v[k] = ql[j][k][ln];    // x | y of entry j
     fe_sqr(t, rho);                            // rho^2
     fe_sel(O1, c, t, odd);                     // x              | rho^2
     fe_sel(O2, bsel, rho, odd);                // beta or 1      | rho
@@ -767,8 +775,7 @@ HKV_DEV void pair_table(const fe& Q, int half, uint32_t odd, uint32_t* __restric
     fe_sel(O1, R, c, odd);                     // beta x         | y
     fe_sel(O2, t, R, odd);                     // rho^2          | rho^3
     fe_mul(R, O1, O2);                         // beta x rho^2   | y rho^3
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ql[j][k][ln] = R.v[k];
+    put(j, R);
   }
 }
 
@@ -997,13 +1004,12 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
   // per chain wave: QTAB_ENTRIES entries x 8 words x 64 lanes (each lane keeps
   // its own coordinate of every entry: x or beta*x on the even lane, y on the odd)
   __shared__ QLane qlds[2];
+  __shared__ HLane hlds[2];
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t shabuf[STD ? 16 * WG : 1];  // std_hash's per-lane SHA-256 blocks ([word][thread])
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
-  const uint32_t n_lanes = gridDim.x * 128u;        // chain lanes of the launch (qs scratch)
-  const uint32_t qlane = blockIdx.x * 128u + (threadIdx.x & 127u);
   // optional phase stamps of workgroup 0 (hkv_profile_phases): constant-rate
   // clock at the phase boundaries of each wave, slot STAMP_*
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
@@ -1052,7 +1058,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
     // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
     fe Zg, Qxy;
     fe_sel(Qxy, q.x, q.y, odd);
-    pair_table(Qxy, half, odd, qs, n_lanes, qlane, qlds[half], ln, Zg);
+    pair_table(Qxy, half, odd, qlds[half], hlds[half], ln, Zg);
     mark(half ? STAMP_TABLE1 : STAMP_TABLE0);
     __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
     if (half == 0) mark(STAMP_P);
@@ -1197,6 +1203,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
                                                                uint32_t* __restrict__ recs, uint32_t mode,
                                                                unsigned long long* __restrict__ clk, StdArgs sa) {
   __shared__ QLane qlds[3];                     // the Q' (wave 0), Q2 (wave 1) and Q1 (wave 3) tables
+  __shared__ HLane hlds[3];                     // their z-ratios while they are built
   __shared__ uint32_t xch[5][25 * BLK_SIGS];    // k2 -> k1 of waves 0, 1, 3; T (0 -> 3); U (3 -> 1)
   __shared__ uint32_t qpub[3][8][BLK_SIGS];     // Q1 = (X, Y, Z), wave 1 -> wave 3
   __shared__ uint32_t shabuf[STD ? 16 * WG : 1];
@@ -1204,8 +1211,6 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
-  const uint32_t n_lanes = gridDim.x * 192u;  // chain lanes of the launch (qs scratch): waves 0, 1, 3
-  const uint32_t qlane = blockIdx.x * 192u + (uint32_t)(wv == 3 ? 2 : wv) * 64u + ln;
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
     if (stamp) clk[4 + slot] = wall_clock64();
@@ -1250,7 +1255,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       key_point<STD>(i, n, recs, sa, q);
       fe_sel(P, q.x, q.y, odd);
       fe_set_u32(zb, 1);
-      pair_table(P, half, odd, qs, n_lanes, qlane, qlds[0], ln, Zg);
+      pair_table(P, half, odd, qlds[0], hlds[0], ln, Zg);
       mark(STAMP_TABLE0);
     } else if (wv == 1) {
       // Q1, Q2 on four lanes per signature (lanes 4c'..4c'+3: X | Y | Z | .)
@@ -1279,7 +1284,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
         P.v[k] = (uint32_t)__shfl((int)V.v[k], src_p);
         zb.v[k] = (uint32_t)__shfl((int)V.v[k], src_z);
       }
-      pair_table(P, half, odd, qs, n_lanes, qlane, qlds[1], ln, Zg);
+      pair_table(P, half, odd, qlds[1], hlds[1], ln, Zg);
       mark(STAMP_TABLE1);
     } else {
       if (ln < BLK_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
@@ -1291,7 +1296,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
         P.v[k] = qpub[odd ? 1 : 0][k][c];
         zb.v[k] = qpub[2][k][c];
       }
-      pair_table(P, half, odd, qs, n_lanes, qlane, qlds[2], ln, Zg);
+      pair_table(P, half, odd, qlds[2], hlds[2], ln, Zg);
     }
     blk_wait(&bflag[BF_SIG], seq);  // the digits, r and flags are in im
     if (wv == 0) mark(STAMP_P);
