@@ -323,7 +323,7 @@ HKV_DEV void fe_quad(fe& r, const fe& a) {
 constexpr int QP_0 = 0x00, QP_1 = 0x55, QP_3 = 0xFF, QP_0112 = 0xD4;  // [0,0,0,0] [1,1,1,1] [3,3,3,3] [0,1,1,3]
 // 2V in the halved form of gej_double (the same point scaled by 1/2)
 HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
-  fe R1, Bq, Aq, E, T, opA, opB, R2, Mq, Cq, E2q, t, X3, D, Y3;
+  fe R1, Bq, Aq, E, T, opA, opB, R2, Mq, E2q, t, X3, D, Y3;
   fe_sqr(R1, V);              // A = X^2 | B = Y^2 | . | .
   fe_quad<QP_1>(Bq, R1);      // B on every lane
   fe_quad<QP_0>(Aq, R1);      // A on every lane
@@ -336,13 +336,12 @@ HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
   fe_sel(opB, opB, Bq, m0 | m1);  // B | B | Z | E'
   fe_mul(R2, opA, opB);       // M = X B | C = B^2 | Z3' = Y Z | E'^2
   fe_quad<QP_0>(Mq, R2);
-  fe_quad<QP_1>(Cq, R2);
   fe_quad<QP_3>(E2q, R2);
   fe_shl(t, Mq, 1);
   fe_sub(X3, E2q, t);         // X3' = E'^2 - 2M
   fe_sub(D, Mq, X3);          // M - X3'
   fe_mul(t, E, D);
-  fe_sub(Y3, t, Cq);          // Y3' = E'(M - X3') - C
+  fe_sub(Y3, t, R2);          // quad lane 1: Y3' = E'(M - X3') - C
   fe_sel(V, R2, Y3, m1);
   fe_sel(V, V, X3, m0);       // X3' | Y3' | Z3' | .
 }

@@ -23,7 +23,8 @@ from collections import defaultdict
 def kname(raw: str) -> str:
     """Kernel name without the namespace / argument list. The ecmult instances:
     round 3 hkv_ecmult_kernel<ILP> (<false> full grid, <true> -> _mid) and
-    hkv_pair_split_kernel<STD> (<false> -> _rec, <true> -> _std); the round-2
+    hkv_pair_split_kernel<STD> / hkv_block_kernel<STD> (<false> -> _rec,
+    <true> -> _std); the round-2
     hkv_ecmult_kernel<SPLIT, ILP> names map as before (<false, false> full
     grid, <false, true> _mid, <true, *> _split)."""
     k = raw.split("(")[0].replace("hkv::", "")
@@ -31,7 +32,7 @@ def kname(raw: str) -> str:
         k = k[5:]
     k = k.replace("<false, false>", "").replace("<false, true>", "_mid")
     k = k.replace("<true, true>", "_split").replace("<true, false>", "_split")
-    if k.startswith("hkv_pair_split_kernel"):
+    if k.startswith("hkv_pair_split_kernel") or k.startswith("hkv_block_kernel"):
         return k.replace("<false>", "_rec").replace("<true>", "_std")
     if k.startswith("hkv_ecmult_kernel"):
         return k.replace("<false>", "").replace("<true>", "_mid")
