@@ -384,6 +384,79 @@ HKV_DEV void pair_add_affine(fe& P, fe& Z, const fe& TXY, uint32_t odd, fe& H) {
   Z = R6;                     //                | Z3
 }
 
+// acc += b for two Jacobian points of one curve in pair form, exact in
+// every case (gej_add_var's semantics): Pa = Xa | Ya, Pb = Xb | Yb, Za and
+// Zb on both lanes, flags pair-uniform. Returns Pa = X3 | Y3 and Za = Z3 on
+// both lanes. 1S + 7M deep — [Zb^2 | Za^2], [U1 = Xa Zb^2 | Za^3],
+// [U2 = Xb Za^2 | Zb^3], [S2 = Yb Za^3 | S1 = Ya Zb^3], [H^2 | Za Zb],
+// [H^3 | V = U1 H^2], [R^2 | Z3 = Za Zb H], [S1 H^3 | R (V - X3)] — against
+// 4S + 12M one lane at a time.
+HKV_DEV void pair_add_var(fe& Pa, fe& Za, bool& ainf, const fe& Pb, const fe& Zb, bool binf, uint32_t odd) {
+  fe O1, O2, T, R1, R2, R3, R4, R5, R6, R7, H, Rr, X3, D, Y3, Pn, Zn;
+  fe_sel(O1, Zb, Za, odd);
+  fe_sqr(R1, O1);             // Zb^2           | Za^2
+  fe_xch(T, R1);              // Za^2           | Zb^2
+  fe_sel(O1, Pa, R1, odd);    // Xa             | Za^2
+  fe_sel(O2, R1, Za, odd);    // Zb^2           | Za
+  fe_mul(R2, O1, O2);         // U1 = Xa Zb^2   | Za^3
+  fe_sel(O1, Pb, T, odd);     // Xb             | Zb^2
+  fe_sel(O2, T, Zb, odd);     // Za^2           | Zb
+  fe_mul(R3, O1, O2);         // U2 = Xb Za^2   | Zb^3
+  fe_xch(T, R2);              // Za^3           | U1
+  fe_xch(O1, Pb);             // Yb             | Xb
+  fe_sel(O1, O1, Pa, odd);    // Yb             | Ya
+  fe_sel(O2, T, R3, odd);     // Za^3           | Zb^3
+  fe_mul(R4, O1, O2);         // S2 = Yb Za^3   | S1 = Ya Zb^3
+  fe_sub(H, R3, R2);          // H = U2 - U1
+  fe_xch(T, R4);              // S1             | S2
+  fe_sub(Rr, R4, T);          // R = S2 - S1
+  const bool live = !ainf && !binf;
+  const bool hz = pair_even(fe_is_zero(H));
+  const bool rz = pair_even(fe_is_zero(Rr));
+  fe_sel(O1, H, Za, odd);     // H              | Za
+  fe_sel(O2, H, Zb, odd);     // H              | Zb
+  fe_mul(R1, O1, O2);         // H^2            | Za Zb
+  fe_xch(T, R1);              // Za Zb          | H^2
+  fe_xch(O2, R2);             // Za^3           | U1
+  fe_sel(O1, H, O2, odd);     // H              | U1
+  fe_sel(O2, R1, T, odd);     // H^2            | H^2
+  fe_mul(R5, O1, O2);         // H^3            | V = U1 H^2
+  fe_xch(T, H);               //                | H
+  fe_sel(O1, Rr, R1, odd);    // R              | Za Zb
+  fe_sel(O2, Rr, T, odd);     // R              | H
+  fe_mul(R6, O1, O2);         // R^2            | Z3 = Za Zb H
+  fe_xch(T, R5);              // V              | H^3
+  fe_sub(X3, R6, R5);
+  fe_shl(O1, T, 1);
+  fe_sub(X3, X3, O1);         // X3 = R^2 - H^3 - 2V
+  fe_sub(D, T, X3);           // V - X3
+  fe_xch(O1, R4);             // S1             | S2
+  fe_xch(T, Rr);              //                | R
+  fe_sel(O1, O1, T, odd);     // S1             | R
+  fe_xch(T, D);               //                | V - X3
+  fe_sel(O2, R5, T, odd);     // H^3            | V - X3
+  fe_mul(R7, O1, O2);         // S1 H^3         | R (V - X3)
+  fe_xch(T, R7);              // R (V - X3)     | S1 H^3
+  fe_sub(Y3, T, R7);          // Y3 = R (V - X3) - S1 H^3
+  fe_xch(T, Y3);
+  fe_sel(Pn, X3, T, odd);     // X3             | Y3
+  fe_bc1(Zn, R6);             // Z3 on both lanes
+  const bool dbl = live && hz && rz, neg = live && hz && !rz;
+  if (__builtin_expect(__any(dbl), 0)) {  // acc == b: 2 acc
+    fe Pd = Pa, Zd = Za, Zd2;
+    pair_double(Pd, Zd, odd);
+    fe_bc1(Zd2, Zd);
+    fe_cmov(Pn, Pd, dbl);
+    fe_cmov(Zn, Zd2, dbl);
+  }
+  const bool take_b = ainf && !binf;
+  fe_cmov(Pa, Pn, live && !neg);
+  fe_cmov(Za, Zn, live && !neg);
+  fe_cmov(Pa, Pb, take_b);
+  fe_cmov(Za, Zb, take_b);
+  ainf = binf ? ainf : (take_b ? false : (live ? neg : ainf));
+}
+
 // (P, Z) := (TXY, 1) on pairs that take a point while at infinity
 HKV_DEV void pair_accumulate_from_inf(fe& P, fe& Z, bool& inf, const fe& TXY, bool take) {
   const bool f = take && inf;

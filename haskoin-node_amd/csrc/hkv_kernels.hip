@@ -1165,33 +1165,39 @@ HKV_DEV void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 // A chain wave's two halves (lanes 0-31 k1, 32-63 k2) summed on the k1
-// lanes: S (valid on the even lanes of 0-31) on the wave's curve
-HKV_DEV void halves_sum(uint32_t* xk, uint32_t c, int half, uint32_t odd, const fe& P, const fe& Z, bool inf, gej& S,
-                        bool& sinf) {
+// lanes in pair form: S = P (X | Y), Z on both lanes, on the wave's curve
+HKV_DEV void halves_sum(uint32_t* xk, uint32_t c, int half, uint32_t odd, fe& P, const fe& Z, bool& inf, fe& Zs) {
   if (half == 1) pair_publish(xk, BLK_SIGS, c, P, Z, inf, odd);
-  fe Y, Zx;
-  fe_xch(Y, P);   // even lane: Y of the pair
-  fe_xch(Zx, Z);  // even lane: Z of the pair
+  fe_bc1(Zs, Z);
   wave_lds_sync();
-  S.x = P;
-  S.y = Y;
-  S.z = Zx;
-  sinf = inf;
   if (half == 0) {
     gej b;
     bool binf;
     xch_read(xk, BLK_SIGS, c, b, binf);
-    gej_add_var(S, sinf, b, binf);
+    fe Pb;
+    fe_sel(Pb, b.x, b.y, odd);
+    pair_add_var(P, Zs, inf, Pb, b.z, binf, odd);
   }
 }
-// acc (on E) += phi^-1 of a segment's sum S: S is Jacobian on E_w at the
-// isomorphic scale zs (its table's Zg times its base point's Z), so on E it
-// is (X, Y, Z zs y0)
-HKV_DEV void add_segment(gej& acc, bool& ainf, gej S, bool sinf, const fe& zs, const fe& y0) {
-  fe zt;
-  fe_mul(zt, S.z, zs);
-  fe_mul(S.z, zt, y0);
-  gej_add_var(acc, ainf, S, sinf);
+// acc (pair form, on E) += phi^-1 of a segment's sum S (pair form): S is
+// Jacobian on E_w at the isomorphic scale zs (its table's Zg times its base
+// point's Z), so on E its Z is Zs zs y0
+HKV_DEV void add_segment(fe& Pacc, fe& Zacc, bool& ainf, const fe& P, const fe& Zs, bool sinf, const fe& zs,
+                         const fe& y0, uint32_t odd) {
+  fe zt, zb;
+  fe_mul(zt, Zs, zs);
+  fe_mul(zb, zt, y0);
+  pair_add_var(Pacc, Zacc, ainf, P, zb, sinf, odd);
+}
+// a pair-form point from / to an LDS exchange slot (X, Y, Z, inf word-major)
+HKV_DEV void pair_from_xch(const uint32_t* xk, uint32_t c, uint32_t odd, fe& P, fe& Z, bool& inf) {
+  gej b;
+  xch_read(xk, BLK_SIGS, c, b, inf);
+  fe_sel(P, b.x, b.y, odd);
+  Z = b.z;
+}
+HKV_DEV void pair_to_xch(uint32_t* xk, uint32_t c, uint32_t odd, const fe& P, const fe& Z, bool inf) {
+  pair_publish(xk, BLK_SIGS, c, P, Z, inf, odd);  // Z is on both lanes: the odd lane's copy is stored
 }
 
 template <bool STD>
@@ -1308,9 +1314,8 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     bool inf;
     pair_chain(P, Z, inf, qlds[slot], im, n_pad, i, valid, negh, half, odd, ln, w_hi, w_lo);
     mark(wv == 0 ? STAMP_CHAIN0 : (wv == 1 ? STAMP_CHAIN1 : STAMP_CHAIN_MID));
-    gej S;
-    bool sinf;
-    halves_sum(xch[slot], c, half, odd, P, Z, inf, S, sinf);  // on E_w at scale Zg * zb
+    fe Zs;
+    halves_sum(xch[slot], c, half, odd, P, Z, inf, Zs);  // S = P | Zs on E_w at scale Zg * zb
     fe zs;
     fe_mul(zs, Zg, zb);
     if (wv == 0) {
@@ -1320,27 +1325,27 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       mark(STAMP_A);
       if (half == 0) {
         gej A;
-        fe y0;
+        fe y0, PA;
         uint32_t r[8], af;
         bool is_sq;
         join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
         bool tinf = (af & AUXF_AINF) != 0;
-        add_segment(A, tinf, S, sinf, zs, y0);
-        if (!odd) xch_write(xch[3], BLK_SIGS, c, A, tinf);
+        fe_sel(PA, A.x, A.y, odd);
+        add_segment(PA, A.z, tinf, P, Zs, inf, zs, y0, odd);
+        pair_to_xch(xch[3], c, odd, PA, A.z, tinf);
       }
       blk_post(&bflag[BF_T], seq);
     } else if (wv == 3) {
       // ---- U = T + phi^-1(S_mid) on E ----
       blk_wait(&bflag[BF_T], seq);
       if (half == 0) {
-        gej T;
+        fe PT, ZT, y0;
         bool tinf;
-        fe y0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
-        xch_read(xch[3], BLK_SIGS, c, T, tinf);
-        add_segment(T, tinf, S, sinf, zs, y0);
-        if (!odd) xch_write(xch[4], BLK_SIGS, c, T, tinf);
+        pair_from_xch(xch[3], c, odd, PT, ZT, tinf);
+        add_segment(PT, ZT, tinf, P, Zs, inf, zs, y0, odd);
+        pair_to_xch(xch[4], c, odd, PT, ZT, tinf);
       }
       blk_post(&bflag[BF_U], seq);
     } else {
@@ -1348,14 +1353,15 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       blk_wait(&bflag[BF_U], seq);
       bool accept = false;
       if (half == 0) {
-        gej A, R;
-        fe y0;
+        gej A;
+        fe y0, PR, ZR;
         uint32_t r[8], af;
         bool is_sq, rinf;
         join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
-        xch_read(xch[4], BLK_SIGS, c, R, rinf);
-        add_segment(R, rinf, S, sinf, zs, y0);
-        accept = valid && is_sq && !rinf && x_matches_r(R.x, R.z, r) && (!STD || (af & AUXF_STDOK));
+        pair_from_xch(xch[4], c, odd, PR, ZR, rinf);
+        add_segment(PR, ZR, rinf, P, Zs, inf, zs, y0, odd);
+        // the even lane holds X
+        accept = valid && is_sq && !rinf && x_matches_r(PR, ZR, r) && (!STD || (af & AUXF_STDOK));
       }
       const uint64_t ball = __ballot(accept && !odd);
       mark(STAMP_JOIN);

@@ -227,6 +227,50 @@ def test_std_inputs_records_and_verdicts_vs_oracle(torch, ver, coracle, forkid):
     assert sum(rej) > 0.8 * len(rej)             # nearly every mutation is rejected (oracle decides which)
 
 
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_std_inputs_block_kernel_small_batches(torch, ver, coracle, forkid):
+    """Batches of 1, 2, 15, 16, 17, 31, 33 and 100 standard inputs take the
+    block kernel (hkv_block_kernel<true>: 16 inputs per workgroup, three chain
+    segments, LDS-flag hand-offs, a 16-bit verdict store per workgroup):
+    partial last workgroups and bitmap half-words shared by two workgroups.
+    Verdicts through the host and the device entry points equal the oracle's
+    on the records the oracle derives; a flipped signature byte rejects
+    exactly its input."""
+    import hkv
+    rng = random.Random(77 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(8)]
+    txs, jobs = txgen.std_block(rng, 90, keys, forkid=forkid, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
+    raw = [sh.tx_serialize(t) for t in txs]
+    parsed = [sh.tx_parse(t) for t in raw]
+    assert len(jobs) >= 100
+    for n in (1, 2, 15, 16, 17, 31, 33, 100):
+        sub = jobs[:n]
+        exp = b"".join(sh.std_input_record(parsed[t], i, p, v, forkid) for (t, i, p, v) in sub)
+        want = oracle_batch(coracle, exp, 1).tolist()
+        assert all(want)
+        assert hkv.verify_std_inputs(ver, raw, sub, forkid) == want
+        assert _device_verify_std(torch, ver, raw, sub, forkid) == want
+    # one bad input in the middle of a 33-input batch (workgroup 1, bit 16 of word 0 / half-word 1)
+    t, i, p, v = jobs[20]
+    tx = sh.tx_parse(raw[t])
+    bad = list(raw)
+    if tx.witness and tx.witness[i]:
+        w = list(tx.witness[i])
+        w[0] = w[0][:7] + bytes([w[0][7] ^ 0x10]) + w[0][8:]
+        tx.witness[i] = w
+    else:
+        items = sh._push_items(tx.inputs[i].script)
+        items[0] = items[0][:7] + bytes([items[0][7] ^ 0x10]) + items[0][8:]
+        tx.inputs[i].script = b"".join(txgen.push(x) for x in items)
+    bad[t] = sh.tx_serialize(tx)
+    got = hkv.verify_std_inputs(ver, bad, jobs[:33], forkid)
+    expect = [True] * 33
+    for k, (tk, ik, _, _) in enumerate(jobs[:33]):
+        if tk == t and ik == i:
+            expect[k] = False
+    assert got == expect
+
+
 def test_std_inputs_bip143_example(ver):
     import hkv
     b = json.load(open(os.path.join(GOLDEN, "bip143_p2wpkh.json")))
