@@ -239,26 +239,34 @@ HKV_DEV void fe_sel(fe& r, const fe& a, const fe& b, uint32_t odd) {
 HKV_DEV bool pair_even(bool f) { return dpp_bc0(f ? 1u : 0u) != 0; }
 HKV_DEV bool pair_odd(bool f) { return dpp_bc1(f ? 1u : 0u) != 0; }
 
-// 2(X, Y, Z) in the halved form of gej_double (the same point scaled by 1/2)
+// 2(X, Y, Z) on a pair (P = X | Y, Z on the odd lane) in the unhalved
+// form with the small multiples gathered into one lane-parallel step: with
+// A = X^2, B = Y^2, M = X B, C = B^2 (dbl-2009-l: E = 3A, S = 4M)
+//   X3 = 9A^2 - 8M,  Y3 = A (36M - 27A^2) - 8C,  Z3 = 2YZ.
+// Products [A | B], [M | YZ], [C | A^2], then [X3 | D] and [8C | 2YZ] side
+// by side (two interleaved small-multiple chains, one shift), [. | A D],
+// [. | Y3]: 2S + 2M deep with two subtractions, where the halved form
+// needed 3A, /2, 2M and three subtractions (tools/ubench_chain.hip).
 HKV_DEV void pair_double(fe& P, fe& Z, uint32_t odd) {
-  fe R1, T, O, R2, E, R3, U, X3, D, t;
-  fe_sqr(R1, P);              // A = X^2        | B = Y^2
+  fe R1, T, O1, R2, R3, X2, X3, P1, P2, u, w, r, Q, t, Y3;
+  fe_sqr(R1, P);              // A              | B
   fe_xch(T, R1);              // B              | A
-  fe_sel(O, T, Z, odd);       // B              | Z
-  fe_mul(R2, P, O);           // M = X B        | Z3' = Y Z
-  fe_mul_small(E, T, 3);
-  fe_half(E, E);              //                | E' = 3A/2
-  fe_sel(O, T, E, odd);       // B              | E'
-  fe_sqr(R3, O);              // C = B^2        | E'^2
-  fe_xch(U, R3);              // E'^2           | C
-  fe_shl(t, R2, 1);
-  fe_sub(X3, U, t);           // X3' = E'^2 - 2M
-  fe_sub(D, R2, X3);          // M - X3'
-  fe_xch(t, D);               //                | M - X3'
-  fe_mul(t, E, t);            //                | E'(M - X3')
-  fe_sub(t, t, U);            //                | Y3' = E'(M - X3') - C
-  fe_sel(P, X3, t, odd);
-  Z = R2;                     //                | Z3'
+  fe_sel(O1, T, Z, odd);      // B              | Z
+  fe_mul(R2, P, O1);          // M = X B        | YZ
+  fe_sqr(R3, T);              // C = B^2        | A^2
+  fe_xch(X2, R2);             // YZ             | M
+  fe_xch(X3, R3);             // A^2            | C
+  fe_sel(P1, X3, X2, odd);    // A^2            | M
+  fe_sel(P2, R2, R3, odd);    // M              | A^2
+  fe_sel(O1, R3, R2, odd);    // C              | YZ
+  fe_mul_small2(u, P1, odd ? 36u : 9u, w, P2, odd ? 27u : 8u);
+  fe_shl_var(Q, O1, odd ? 1u : 3u);   // 8C | 2YZ
+  fe_sub(r, u, w);            // X3             | D = 36M - 27A^2
+  fe_mul(t, T, r);            //                | A D
+  fe_xch(O1, Q);              //                | 8C
+  fe_sub(Y3, t, O1);          //                | Y3
+  fe_sel(P, r, Y3, odd);
+  Z = Q;                      //                | Z3
 }
 
 // The pair form of gej_accumulate: (P, Z, inf) += T with T = TXY = tx (even
@@ -310,9 +318,8 @@ HKV_DEV void pair_accumulate(fe& P, fe& Z, bool& inf, const fe& TXY, bool take, 
   }
 }
 // ---- quad-lane form: one point on four lanes (4c .. 4c + 3) ----
-// V = X | Y | Z | (unused) on quad lanes 0..3. A doubling is S + 2M deep:
-// [X^2 | Y^2], then [X B | B^2 | Y Z | E'^2] on all four lanes, then
-// [E'(M - X3')] — against 2S + 2M in the pair form. Operands move by DPP
+// V = X | Y | Z | (unused) on quad lanes 0..3. A doubling is S + 2M deep
+// against 2S + 2M in the pair form. Operands move by DPP
 // quad permutations (quad_perm [s0, s1, s2, s3]: lane q reads lane s_q of
 // its quad) and lane-mask selects (m0, m1, m2: all ones on quad lane 0, 1, 2).
 template <int PERM>
@@ -321,29 +328,36 @@ HKV_DEV void fe_quad(fe& r, const fe& a) {
   for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], PERM, 0xF, 0xF, false);
 }
 constexpr int QP_0 = 0x00, QP_1 = 0x55, QP_3 = 0xFF, QP_0112 = 0xD4;  // [0,0,0,0] [1,1,1,1] [3,3,3,3] [0,1,1,3]
-// 2V in the halved form of gej_double (the same point scaled by 1/2)
+// 2V in the unhalved form of pair_double: [A | B | . | .], then
+// [M | C | YZ | A^2] on the four lanes, [X3 | D | Z3 | 8C] by two
+// interleaved small-multiple chains and one subtraction, [. | A D | . | .],
+// [. | Y3 | . | .]: S + 2M deep.
 HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
-  fe R1, Bq, Aq, E, T, opA, opB, R2, Mq, E2q, t, X3, D, Y3;
+  fe R1, Aq, Bq, T, opA, opB, R2, Mq, Cq, A2q, P1, P2, u, w, r, t, C8, Y3;
   fe_sqr(R1, V);              // A = X^2 | B = Y^2 | . | .
-  fe_quad<QP_1>(Bq, R1);      // B on every lane
-  fe_quad<QP_0>(Aq, R1);      // A on every lane
-  fe_mul_small(E, Aq, 3);
-  fe_half(E, E);              // E' = 3A/2
+  fe_quad<QP_0>(Aq, R1);
+  fe_quad<QP_1>(Bq, R1);
   fe_quad<QP_0112>(T, V);     // X | . | Y | .
-  fe_sel(opA, E, Bq, m1);
-  fe_sel(opA, opA, T, m0 | m2);   // X | B | Y | E'
-  fe_sel(opB, E, V, m2);
-  fe_sel(opB, opB, Bq, m0 | m1);  // B | B | Z | E'
-  fe_mul(R2, opA, opB);       // M = X B | C = B^2 | Z3' = Y Z | E'^2
+  fe_sel(opA, Aq, Bq, m1);
+  fe_sel(opA, opA, T, m0 | m2);   // X | B | Y | A
+  fe_sel(opB, Aq, V, m2);
+  fe_sel(opB, opB, Bq, m0 | m1);  // B | B | Z | A
+  fe_mul(R2, opA, opB);       // M | C | YZ | A^2
   fe_quad<QP_0>(Mq, R2);
-  fe_quad<QP_3>(E2q, R2);
-  fe_shl(t, Mq, 1);
-  fe_sub(X3, E2q, t);         // X3' = E'^2 - 2M
-  fe_sub(D, Mq, X3);          // M - X3'
-  fe_mul(t, E, D);
-  fe_sub(Y3, t, R2);          // quad lane 1: Y3' = E'(M - X3') - C
-  fe_sel(V, R2, Y3, m1);
-  fe_sel(V, V, X3, m0);       // X3' | Y3' | Z3' | .
+  fe_quad<QP_1>(Cq, R2);
+  fe_quad<QP_3>(A2q, R2);
+  fe_sel(P1, Cq, R2, m2);
+  fe_sel(P1, P1, Mq, m1);
+  fe_sel(P1, P1, A2q, m0);    // A^2 | M | YZ | C
+  fe_sel(P2, A2q, Mq, m0);    // M | A^2 | . | .
+  const uint32_t k1 = m0 ? 9u : (m1 ? 36u : (m2 ? 2u : 8u));
+  const uint32_t k2 = m0 ? 8u : (m1 ? 27u : 0u);
+  fe_mul_small2(u, P1, k1, w, P2, k2);
+  fe_sub(r, u, w);            // X3 | D = 36M - 27A^2 | Z3 = 2YZ | 8C
+  fe_mul(t, Aq, r);           // . | A D | . | .
+  fe_quad<QP_3>(C8, r);
+  fe_sub(Y3, t, C8);          // . | Y3 | . | .
+  fe_sel(V, r, Y3, m1);       // X3 | Y3 | Z3 | .
 }
 
 // P += TXY in place for a table build: TXY affine on the curve of the
