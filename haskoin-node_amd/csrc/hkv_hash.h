@@ -16,6 +16,13 @@ namespace hkv {
 
 HKV_DEV uint32_t rotr32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 HKV_DEV uint32_t rotl32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one instruction, the
+// immediate its truth table over (a, b, c) = (0xF0, 0xCC, 0xAA). The compiler
+// forms it for Ch / Maj but leaves the Sigma functions' XOR of three
+// rotations as two v_xor_b32.
+HKV_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+HKV_DEV uint32_t sha_ch(uint32_t e, uint32_t f, uint32_t g) { return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA); }
+HKV_DEV uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8); }
 
 HKV_DEV void sha256_init(uint32_t h[8]) {
   h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
@@ -41,15 +48,15 @@ HKV_DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
       wt = w[t];
     } else {
       const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wt = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
     }
-    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t ch = sha_ch(e, f, g);
     const uint32_t t1 = hh + S1 + ch + K[t] + wt;
-    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    const uint32_t mj = sha_maj(a, b, c);
     hh = g; g = f; f = e; e = d + t1;
     d = c; c = b; b = a; a = t1 + S0 + mj;
   }

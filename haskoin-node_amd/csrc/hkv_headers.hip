@@ -8,13 +8,15 @@
 // that the header extends its predecessor. Those three are independent per
 // header and run here, one lane per header:
 //
-//   hkv_header_hash_kernel  SHA-256d (2 + 1 compressions), decodeCompact of
-//                           the bits field, isValidPOW against powLimit.
-//   hkv_header_link_kernel  prev field of header i == hash of header i-1
-//                           (header 0 against the caller's tip hash).
+//   hkv_header_kernel  SHA-256d (2 + 1 compressions), decodeCompact of the
+//                      bits field, isValidPOW against powLimit, and the prev
+//                      field of header i == hash of header i-1 (header 0
+//                      against the caller's tip hash), the predecessor's hash
+//                      read from LDS.
 //
-// Memory: a workgroup's 256 headers (20,480 contiguous bytes) are staged into
-// LDS by coalesced dword loads, then each lane reads its own 20 words. The
+// Memory: a workgroup's 256 headers (20,480 contiguous bytes: its 255 own and
+// the one before them) are staged into LDS by coalesced dword loads, then each
+// lane reads its own 20 words. The
 // work is 3 SHA-256 compressions per 80-byte header: latency- and ALU-light,
 // far below both the VALU and HBM rooflines at sync batch sizes (a 2,000-
 // header message is 160 KB); DESIGN.md records the measured rate.
@@ -62,75 +64,89 @@ HKV_DEV bool u256_gt(const uint32_t a[8], const uint32_t b[8]) {
   return gt;
 }
 
-__global__ void __launch_bounds__(WG) hkv_header_hash_kernel(const uint32_t* __restrict__ hdrs, uint32_t n,
-                                                             const uint32_t* __restrict__ pow_limit,
-                                                             uint32_t* __restrict__ hashes,
-                                                             uint8_t* __restrict__ status) {
+// One workgroup owns HDR_OWN = WG - 1 consecutive headers: lane t hashes
+// header base - 1 + t, so lane 0 recomputes the last header of the previous
+// workgroup (in workgroup 0 it idles and header 0 links against the caller's
+// tip) and every prev-field check reads its predecessor's hash from LDS. One
+// launch instead of a hash kernel and a link kernel that re-read the hashes,
+// at 1/256 extra hashing.
+constexpr uint32_t HDR_OWN = WG - 1;
+
+__global__ void __launch_bounds__(WG) hkv_header_kernel(const uint32_t* __restrict__ hdrs, uint32_t n,
+                                                        const uint32_t* __restrict__ pow_limit,
+                                                        const uint32_t* __restrict__ prev0,
+                                                        uint32_t* __restrict__ hashes, uint8_t* __restrict__ status) {
   __shared__ uint32_t lds[WG * HDR_WORDS];
-  const uint32_t base = blockIdx.x * WG;
-  const uint32_t cnt = min((uint32_t)WG, n - base);
-  const uint32_t* src = hdrs + (size_t)base * HDR_WORDS;
-  for (uint32_t k = threadIdx.x; k < cnt * HDR_WORDS; k += WG) lds[k] = src[k];
+  __shared__ uint32_t lh[WG * 8];
+  const uint32_t t = threadIdx.x;
+  const uint32_t base = blockIdx.x * HDR_OWN;  // the first header this workgroup owns (lane 1)
+  const uint32_t s0 = blockIdx.x == 0 ? 1u : 0u;  // workgroup 0 has no predecessor slot
+  const uint32_t first = base + s0 - 1;          // header in slot s0
+  const uint32_t last = min(base + HDR_OWN, n);  // one past the last staged header
+  const uint32_t cnt = last - first;
+  const uint32_t* src = hdrs + (size_t)first * HDR_WORDS;
+  uint32_t* dst = lds + s0 * HDR_WORDS;
+  for (uint32_t k = t; k < cnt * HDR_WORDS; k += WG) dst[k] = src[k];
   __syncthreads();
-  const uint32_t i = base + threadIdx.x;
-  if (threadIdx.x >= cnt) return;
-  uint32_t h[HDR_WORDS];
+  // slot t holds header base - 1 + t
+  const bool staged = t >= s0 && t < s0 + cnt;
+  const uint32_t i = base + t - 1;
+  uint32_t h[HDR_WORDS], hv[8];
+  uint32_t fl = 0;
+  if (staged) {
 #pragma unroll
-  for (int k = 0; k < HDR_WORDS; ++k) h[k] = lds[threadIdx.x * HDR_WORDS + k];
+    for (int k = 0; k < HDR_WORDS; ++k) h[k] = lds[t * HDR_WORDS + k];
 
-  // SHA-256 of the 80 bytes: block 1 = words 0..15, block 2 = words 16..19 + padding
-  uint32_t st[8], w[16];
-  sha256_init(st);
+    // SHA-256 of the 80 bytes: block 1 = words 0..15, block 2 = words 16..19 + padding
+    uint32_t st[8], w[16];
+    sha256_init(st);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = __builtin_bswap32(h[k]);
-  sha256_compress(st, w);
+    for (int k = 0; k < 16; ++k) w[k] = __builtin_bswap32(h[k]);
+    sha256_compress(st, w);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) w[k] = __builtin_bswap32(h[16 + k]);
-  w[4] = 0x80000000u;
+    for (int k = 0; k < 4; ++k) w[k] = __builtin_bswap32(h[16 + k]);
+    w[4] = 0x80000000u;
 #pragma unroll
-  for (int k = 5; k < 15; ++k) w[k] = 0;
-  w[15] = 640;
-  sha256_compress(st, w);
-  uint32_t d[8];
-  sha256_of_digest(d, st);
+    for (int k = 5; k < 15; ++k) w[k] = 0;
+    w[15] = 640;
+    sha256_compress(st, w);
+    uint32_t d[8];
+    sha256_of_digest(d, st);
 
-  // headerHash bytes in digest order == little-endian limbs of headerPOW
-  uint32_t hv[8];
+    // headerHash bytes in digest order == little-endian limbs of headerPOW
 #pragma unroll
-  for (int k = 0; k < 8; ++k) hv[k] = __builtin_bswap32(d[k]);
-  uint32_t* out = hashes + (size_t)i * 8;
-#pragma unroll
-  for (int k = 0; k < 8; k += 4) *reinterpret_cast<uint4*>(out + k) = make_uint4(hv[k], hv[k + 1], hv[k + 2], hv[k + 3]);
+    for (int k = 0; k < 8; ++k) {
+      hv[k] = __builtin_bswap32(d[k]);
+      lh[t * 8 + k] = hv[k];
+    }
 
-  // isValidPOW
-  uint32_t tgt[8], lim[8];
-  uint32_t fl = decode_compact(h[18], tgt);
+    // isValidPOW
+    uint32_t tgt[8], lim[8];
+    fl = decode_compact(h[18], tgt);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) lim[k] = pow_limit[k];
-  if (!(fl & HKV_HDR_OVERFLOW)) {
-    if (u256_gt(tgt, lim)) fl |= HKV_HDR_ABOVE_LIMIT;
-    if (u256_gt(hv, tgt)) fl |= HKV_HDR_HASH_ABOVE;
+    for (int k = 0; k < 8; ++k) lim[k] = pow_limit[k];
+    if (!(fl & HKV_HDR_OVERFLOW)) {
+      if (u256_gt(tgt, lim)) fl |= HKV_HDR_ABOVE_LIMIT;
+      if (u256_gt(hv, tgt)) fl |= HKV_HDR_HASH_ABOVE;
+    }
+    if (!(fl & (HKV_HDR_NEGATIVE | HKV_HDR_OVERFLOW | HKV_HDR_ZERO_TARGET | HKV_HDR_ABOVE_LIMIT | HKV_HDR_HASH_ABOVE)))
+      fl |= HKV_HDR_POW_OK;
   }
-  if (!(fl & (HKV_HDR_NEGATIVE | HKV_HDR_OVERFLOW | HKV_HDR_ZERO_TARGET | HKV_HDR_ABOVE_LIMIT | HKV_HDR_HASH_ABOVE)))
-    fl |= HKV_HDR_POW_OK;
-  status[i] = (uint8_t)fl;
-}
-
-// prev field (words 1..8) of header i against the hash of header i-1
-__global__ void __launch_bounds__(WG) hkv_header_link_kernel(const uint32_t* __restrict__ hdrs, uint32_t n,
-                                                             const uint32_t* __restrict__ prev0,
-                                                             const uint32_t* __restrict__ hashes,
-                                                             uint8_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t* p = hdrs + (size_t)i * HDR_WORDS + 1;
-  const uint32_t* q = i ? hashes + (size_t)(i - 1) * 8 : prev0;
+  __syncthreads();
+  if (!staged || t == 0) return;  // lane 0 only supplied its hash
+  // prev field (words 1..8) against the hash of header i - 1 (header 0:
+  // the caller's tip, or linked by definition without one)
+  const uint32_t* q = i ? lh + (t - 1) * 8 : prev0;
   uint32_t diff = 0;
   if (q) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) diff |= p[k] ^ q[k];
+    for (int k = 0; k < 8; ++k) diff |= h[1 + k] ^ q[k];
   }
-  if (diff == 0) status[i] = (uint8_t)(status[i] | HKV_HDR_LINK_OK);
+  if (diff == 0) fl |= HKV_HDR_LINK_OK;
+  uint32_t* out = hashes + (size_t)i * 8;
+#pragma unroll
+  for (int k = 0; k < 8; k += 4) *reinterpret_cast<uint4*>(out + k) = make_uint4(hv[k], hv[k + 1], hv[k + 2], hv[k + 3]);
+  status[i] = (uint8_t)fl;
 }
 
 // ---------------------------------------------------------------------------
@@ -369,13 +385,10 @@ hipError_t launch_merkle(const uint8_t* leaves, const uint32_t* offsets, uint32_
 hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
                           uint8_t* hashes, uint8_t* status, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const uint32_t blocks = (n + WG - 1) / WG;
-  hipLaunchKernelGGL(hkv_header_hash_kernel, dim3(blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(hdrs),
-                     n, reinterpret_cast<const uint32_t*>(pow_limit), reinterpret_cast<uint32_t*>(hashes), status);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(hkv_header_link_kernel, dim3(blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(hdrs),
-                     n, reinterpret_cast<const uint32_t*>(prev0), reinterpret_cast<const uint32_t*>(hashes), status);
+  const uint32_t blocks = (n + HDR_OWN - 1) / HDR_OWN;
+  hipLaunchKernelGGL(hkv_header_kernel, dim3(blocks), dim3(WG), 0, st, reinterpret_cast<const uint32_t*>(hdrs), n,
+                     reinterpret_cast<const uint32_t*>(pow_limit), reinterpret_cast<const uint32_t*>(prev0),
+                     reinterpret_cast<uint32_t*>(hashes), status);
   return hipGetLastError();
 }
 

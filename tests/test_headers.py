@@ -152,7 +152,7 @@ def test_gpu_fixture_chain(verifier):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 63, 255, 256, 257, 2000, 5003])
+@pytest.mark.parametrize("n", [1, 63, 255, 256, 257, 510, 511, 2000, 5003])
 def test_gpu_random_headers_parity(verifier, n):
     import hkv
     hdrs = make_headers(n, seed=0x48445200 + n)
