@@ -248,16 +248,14 @@ HKV_DEV bool pair_odd(bool f) { return dpp_bc1(f ? 1u : 0u) != 0; }
 // [. | Y3]: 2S + 2M deep with two subtractions, where the halved form
 // needed 3A, /2, 2M and three subtractions (tools/ubench_chain.hip).
 HKV_DEV void pair_double(fe& P, fe& Z, uint32_t odd) {
-  fe R1, T, O1, R2, R3, X2, X3, P1, P2, u, w, r, Q, t, Y3;
+  fe R1, T, O1, R2, R3, P1, P2, u, w, r, Q, t, Y3;
   fe_sqr(R1, P);              // A              | B
   fe_xch(T, R1);              // B              | A
   fe_sel(O1, T, Z, odd);      // B              | Z
   fe_mul(R2, P, O1);          // M = X B        | YZ
   fe_sqr(R3, T);              // C = B^2        | A^2
-  fe_xch(X2, R2);             // YZ             | M
-  fe_xch(X3, R3);             // A^2            | C
-  fe_sel(P1, X3, X2, odd);    // A^2            | M
   fe_sel(P2, R2, R3, odd);    // M              | A^2
+  fe_xch(P1, P2);             // A^2            | M
   fe_sel(O1, R3, R2, odd);    // C              | YZ
   fe_mul_small2(u, P1, odd ? 36u : 9u, w, P2, odd ? 27u : 8u);
   fe_shl_var(Q, O1, odd ? 1u : 3u);   // 8C | 2YZ
@@ -327,29 +325,25 @@ HKV_DEV void fe_quad(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], PERM, 0xF, 0xF, false);
 }
-constexpr int QP_0 = 0x00, QP_1 = 0x55, QP_3 = 0xFF, QP_0112 = 0xD4;  // [0,0,0,0] [1,1,1,1] [3,3,3,3] [0,1,1,3]
+constexpr int QP_0 = 0x00, QP_3 = 0xFF, QP_0112 = 0xD4;  // [0,0,0,0] [3,3,3,3] [0,1,1,3]
+constexpr int QP_1100 = 0x05, QP_3021 = 0x63, QP_0333 = 0xFC;  // [1,1,0,0] [3,0,2,1] [0,3,3,3]
 // 2V in the unhalved form of pair_double: [A | B | . | .], then
 // [M | C | YZ | A^2] on the four lanes, [X3 | D | Z3 | 8C] by two
 // interleaved small-multiple chains and one subtraction, [. | A D | . | .],
-// [. | Y3 | . | .]: S + 2M deep.
+// [. | Y3 | . | .]: S + 2M deep. Operands that are one quad permutation of a
+// product are formed by a single DPP move per limb (P1, P2), and the others
+// by two permutations and one select, not by broadcasts and select chains.
 HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
-  fe R1, Aq, Bq, T, opA, opB, R2, Mq, Cq, A2q, P1, P2, u, w, r, t, C8, Y3;
+  fe R1, Aq, RA, T, opA, opB, R2, P1, P2, u, w, r, t, C8, Y3;
   fe_sqr(R1, V);              // A = X^2 | B = Y^2 | . | .
-  fe_quad<QP_0>(Aq, R1);
-  fe_quad<QP_1>(Bq, R1);
-  fe_quad<QP_0112>(T, V);     // X | . | Y | .
-  fe_sel(opA, Aq, Bq, m1);
-  fe_sel(opA, opA, T, m0 | m2);   // X | B | Y | A
-  fe_sel(opB, Aq, V, m2);
-  fe_sel(opB, opB, Bq, m0 | m1);  // B | B | Z | A
+  fe_quad<QP_0>(Aq, R1);      // A        | A      | A  | A
+  fe_quad<QP_1100>(RA, R1);   // B        | B      | A  | A
+  fe_quad<QP_0112>(T, V);     // X        | .      | Y  | .
+  fe_sel(opA, RA, T, m0 | m2);    // X | B | Y | A
+  fe_sel(opB, RA, V, m2);         // B | B | Z | A
   fe_mul(R2, opA, opB);       // M | C | YZ | A^2
-  fe_quad<QP_0>(Mq, R2);
-  fe_quad<QP_1>(Cq, R2);
-  fe_quad<QP_3>(A2q, R2);
-  fe_sel(P1, Cq, R2, m2);
-  fe_sel(P1, P1, Mq, m1);
-  fe_sel(P1, P1, A2q, m0);    // A^2 | M | YZ | C
-  fe_sel(P2, A2q, Mq, m0);    // M | A^2 | . | .
+  fe_quad<QP_3021>(P1, R2);   // A^2 | M | YZ | C
+  fe_quad<QP_0333>(P2, R2);   // M | A^2 | . | .
   const uint32_t k1 = m0 ? 9u : (m1 ? 36u : (m2 ? 2u : 8u));
   const uint32_t k2 = m0 ? 8u : (m1 ? 27u : 0u);
   fe_mul_small2(u, P1, k1, w, P2, k2);
