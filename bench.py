@@ -3,6 +3,12 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+Without a launcher (WORLD_SIZE unset), --gpus N > 1 starts N rank processes
+itself (fresh interpreters with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*; the
+parent makes no GPU call) and exits non-zero at once when fewer than N GPUs
+are visible. Under torchrun --gpus must equal WORLD_SIZE. The line carries
+`ranks_seen` (dist.get_world_size()) and every rank's device.
+
 Workloads (records generated on device by the keyless construction, 90%
 compressed / 10% uncompressed keys from a 65,536-key pool, low-S, resident in
 HBM before the timed region):
@@ -476,9 +482,128 @@ def load_traffic(path: str, n: int):
     return 2 * f + w, {"fetch_size_bytes": f, "write_size_bytes": w, "source": tj.get("source")}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices() -> int:
+    """GPUs this process may use. torch.cuda.device_count() does not
+    initialise the GPU on this image, so the launcher may call it before it
+    starts the ranks."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def spawn_ranks(n: int, argv: list, mock: bool = False) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes
+    (fresh interpreters, never an exec of this one) with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set as torchrun would, wait for all of them and
+    return the first non-zero exit code (the others are then killed by PID).
+    Rank 0 prints the JSON line on the inherited stdout. The parent makes no
+    GPU call; it fails fast when fewer than N devices are visible."""
+    import subprocess
+    if not mock:
+        have = visible_devices()
+        if n > have:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HKV_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank process {p.pid} exited with {code}; stopping the others", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+def mock_pattern(k):
+    """Verdict of global record k in the CPU mock leg (a fixed bit pattern:
+    the launcher test checks the gathered bitmap against it)."""
+    import numpy as np
+    k = np.asarray(k, dtype=np.uint64)
+    return ((k * np.uint64(2654435761)) >> np.uint64(7)) & np.uint64(1)
+
+
+def mock_main(args, world: int, rank: int) -> None:
+    """The launcher and the multi-rank step on CPU (gloo): the same
+    ShardedVerify, barrier, timing and max-over-ranks reduction as the GPU
+    run, with a pattern writer instead of hkv_verify_device. For tests only
+    (`--mock-cpu`); it prints a line marked "mock": true."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "haskoin-node_amd"))
+    from hkv.records import bits_from_bools
+    from hkv.shard import ShardedVerify
+    if world > 1:
+        dist.init_process_group("gloo")
+    if os.environ.get("HKV_MOCK_FAIL_RANK") == str(rank):
+        sys.exit(3)  # test hook: this rank dies inside the group, the others block in the all-gather
+    n_total = args.config4_n
+
+    def verify(lo, hi, bits):
+        w = bits_from_bools(mock_pattern(np.arange(lo, hi)).astype(bool))
+        bits.zero_()
+        bits[: len(w)] = torch.from_numpy(w.view(np.int32))
+
+    sv = ShardedVerify(torch, n_total, rank, world, verify, dist=dist, device="cpu")
+    for _ in range(args.warmup):
+        sv.step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sv.step()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    full = sv.bitmap()
+    lab = bits_from_bools(mock_pattern(np.arange(sv.lo, sv.hi)).astype(bool))
+    chk = torch.tensor([sv.slice_mismatches(full, lab)], dtype=torch.int64)
+    devs = [{"rank": rank, "device": "cpu", "pid": os.getpid()}]
+    if world > 1:
+        dist.all_reduce(chk, op=dist.ReduceOp.SUM)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, devs[0])
+        devs = gathered
+    if rank == 0:
+        dt = t.item()
+        print(json.dumps({"metric": "mock", "mock": True, "value": round(n_total * args.steps / dt, 1),
+                          "n_gpus": world, "ranks_seen": world, "rank_devices": devs, "steps": args.steps,
+                          "warmup": args.warmup, "mismatches": int(chk.item()), "global_batch": n_total}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each). Without a launcher (WORLD_SIZE unset) N > 1 starts N rank processes; "
+                         "under torchrun it must equal WORLD_SIZE")
+    ap.add_argument("--mock-cpu", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--per-gpu", type=int, default=PER_GPU)
@@ -497,13 +622,28 @@ def main() -> None:
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], mock=args.mock_cpu))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr,
+              flush=True)
+        sys.exit(2)
+    if args.mock_cpu:
+        mock_main(args, world, rank)
+        return
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    have = torch.cuda.device_count()
+    if local >= have:
+        print(f"bench.py: rank {rank} needs GPU {local} but only {have} visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -583,6 +723,17 @@ def main() -> None:
     if world > 1:
         dist.all_reduce(chk, op=dist.ReduceOp.SUM)
     mismatches, accepted, label_valid = chk.tolist()
+    # which device every rank ran on (the line proves N ranks on N GPUs)
+    props = torch.cuda.get_device_properties(local)
+    me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(), "name": props.name,
+          "pci_bus_id": getattr(props, "pci_bus_id", None), "pci_device_id": getattr(props, "pci_device_id", None),
+          "uuid": str(getattr(props, "uuid", "")) or None, "pid": os.getpid(), "local_n": n}
+    rank_devices = [me]
+    ranks_seen = 1
+    if world > 1:
+        ranks_seen = dist.get_world_size()
+        rank_devices = [None] * world
+        dist.all_gather_object(rank_devices, me)
 
     if rank == 0:
         value = n_total * args.steps / dt_max
@@ -637,6 +788,11 @@ def main() -> None:
             "value": round(value, 1),
             "unit": "verifies/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "rank_devices": rank_devices,
+            "launcher": ("bench.py spawn" if os.environ.get("HKV_BENCH_SPAWNED") else
+                         "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or "GROUP_RANK" in os.environ else
+                         "external" if world > 1 else "single process"),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 4),

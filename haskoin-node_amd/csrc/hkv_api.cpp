@@ -109,6 +109,12 @@ int hip_fail(hipError_t e, const char* what) {
   g_last_hip = std::string(what) + ": " + hipGetErrorString(e);
   return HKV_E_HIP;
 }
+// an allocation (or other resource) failure: the call's error, not a fault of
+// the device (hkv_plan.h is_device_fault: it does not make failover re-shard)
+int oom_fail(hipError_t e, const char* what) {
+  g_last_hip = std::string(what) + ": " + hipGetErrorString(e);
+  return HKV_E_OOM;
+}
 #define HKV_TRY(expr, what)                       \
   do {                                            \
     hipError_t e_ = (expr);                       \
@@ -627,6 +633,13 @@ int hkv_device_healthy(hkv_ctx* ctx, int dev) {
   return ctx->healthy[(size_t)dev] ? 1 : 0;
 }
 
+int hkv_device_reset_health(hkv_ctx* ctx, int dev) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  ctx->healthy[(size_t)dev] = true;
+  return HKV_OK;
+}
+
 int hkv_device_failures(hkv_ctx* ctx, int dev) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return HKV_E_ARG;
   std::lock_guard<std::mutex> lock(ctx->mu);
@@ -634,7 +647,7 @@ int hkv_device_failures(hkv_ctx* ctx, int dev) {
 }
 
 int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when) {
-  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || when > HKV_FAIL_JOIN) return HKV_E_ARG;
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || when > HKV_FAIL_ALLOC) return HKV_E_ARG;
   std::lock_guard<std::mutex> lock(ctx->mu);
   ctx->devs[(size_t)dev].inject = when;
   return HKV_OK;
@@ -686,6 +699,10 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
     g_last_hip = "injected enqueue failure (hkv_debug_fail_device)";
     return HKV_E_HIP;
   }
+  if (d.inject == HKV_FAIL_ALLOC) {
+    d.inject = 0;
+    return oom_fail(hipErrorOutOfMemory, "injected allocation failure (hkv_debug_fail_device)");
+  }
   const size_t len = s.hi - s.lo;
   hipError_t e0 = hipSetDevice(d.device);
   int rc = e0 == hipSuccess ? scratch_acquire(d, d.stream) : hip_fail(e0, "hipSetDevice");
@@ -695,7 +712,7 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
     d.recs = nullptr;
     d.recs_cap = 0;
     e0 = hipMalloc(&d.recs, len * hkv::REC_SIZE);
-    if (e0 != hipSuccess) rc = hip_fail(e0, "hipMalloc(records)");
+    if (e0 != hipSuccess) rc = oom_fail(e0, "hipMalloc(records)");
     else d.recs_cap = len;
   }
   const size_t words = (len + 31) / 32;
@@ -704,7 +721,7 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
     d.hbits = nullptr;
     d.hbits_cap = 0;
     e0 = hipHostMalloc(reinterpret_cast<void**>(&d.hbits), words * 4, hipHostMallocPortable);
-    if (e0 != hipSuccess) rc = hip_fail(e0, "hipHostMalloc(bits)");
+    if (e0 != hipSuccess) rc = oom_fail(e0, "hipHostMalloc(bits)");
     else d.hbits_cap = words;
   }
   if (rc) return rc;
@@ -715,7 +732,11 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
     const size_t cl = std::min(chunk, len - off);
     hipEvent_t ev = nullptr;
     hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e == hipSuccess) evs.push_back(ev);
+    if (e != hipSuccess) {
+      rc = oom_fail(e, "hipEventCreate");
+      break;
+    }
+    evs.push_back(ev);
     if (e == hipSuccess)
       e = hipMemcpyAsync(d.recs + off * hkv::REC_SIZE, src + off * hkv::REC_SIZE, cl * hkv::REC_SIZE,
                          hipMemcpyHostToDevice, d.copy_stream);

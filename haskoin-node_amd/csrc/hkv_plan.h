@@ -54,17 +54,27 @@ inline bool merge_shard_words(uint32_t* out, size_t out_words, const uint32_t* w
   return true;
 }
 
+// Only a HIP runtime error from the device's own streams, launches or
+// synchronisation (HKV_E_HIP = -4) says the device is bad. Allocation
+// failures (HKV_E_OOM), argument and internal errors are the call's, not the
+// device's: re-sharding them onto the other devices would need even larger
+// buffers there, so one out-of-memory would cascade over every device.
+inline bool is_device_fault(int rc) { return rc == -4; }
+
 // Run [0, n) over the healthy devices with failover. enqueue(shard) starts a
 // shard on its device and returns 0 or an error; join(shard) waits for it
 // and merges its verdicts, returning 0 or an error. A round starts at most
 // one shard per device (a device's staging buffers hold one shard) and joins
-// every shard it started. A device whose enqueue or join fails is marked
-// unhealthy (healthy[dev] = false), and its shards — the failed one and any
-// still queued for it — are re-planned over the devices still healthy,
-// round after round, until all of [0, n) is verified (returns 0) or no
-// healthy device is left (returns the last error, or -2 = HKV_E_NODEV when
-// none was healthy to begin with). Shards that completed are never re-run.
-// on_fail(dev, rc) is told about each device's first failure.
+// every shard it started. A device whose enqueue or join fails with a device
+// fault (is_device_fault) is marked unhealthy (healthy[dev] = false), and its
+// shards — the failed one and any still queued for it — are re-planned over
+// the devices still healthy, round after round, until all of [0, n) is
+// verified (returns 0) or no healthy device is left (returns the last error,
+// or -2 = HKV_E_NODEV when none was healthy to begin with). Shards that
+// completed are never re-run. on_fail(dev, rc) is told about each device's
+// first failure. Any other error ends the call: no further shard is started,
+// the shards already started are joined (their copies still read the
+// caller's records), no device changes health, and that error is returned.
 template <class Enqueue, class Join, class OnFail>
 int run_with_failover(size_t n, std::vector<bool>& healthy, Enqueue enqueue, Join join, OnFail on_fail) {
   auto healthy_devs = [&]() {
@@ -82,6 +92,7 @@ int run_with_failover(size_t n, std::vector<bool>& healthy, Enqueue enqueue, Joi
     if (healthy[(size_t)dev]) on_fail(dev, rc);
     healthy[(size_t)dev] = false;
   };
+  int abort_rc = 0;  // first non-device error: the call ends after this round's joins
   while (!todo.empty()) {
     std::vector<Shard> round, rest, started, failed;
     std::vector<bool> busy(healthy.size(), false);
@@ -94,8 +105,10 @@ int run_with_failover(size_t n, std::vector<bool>& healthy, Enqueue enqueue, Joi
       }
     }
     for (const Shard& s : round) {
+      if (abort_rc) break;
       const int rc = healthy[(size_t)s.dev] ? enqueue(s) : 0;
       if (!healthy[(size_t)s.dev]) failed.push_back(s);
+      else if (rc && !is_device_fault(rc)) abort_rc = rc;
       else if (rc) {
         fail(s.dev, rc);
         failed.push_back(s);
@@ -105,11 +118,14 @@ int run_with_failover(size_t n, std::vector<bool>& healthy, Enqueue enqueue, Joi
     }
     for (const Shard& s : started) {
       const int rc = join(s);
-      if (rc) {
+      if (rc && !is_device_fault(rc)) {
+        if (!abort_rc) abort_rc = rc;
+      } else if (rc) {
         fail(s.dev, rc);
         failed.push_back(s);
       }
     }
+    if (abort_rc) return abort_rc;
     todo.clear();
     for (const Shard& s : rest) (healthy[(size_t)s.dev] ? todo : failed).push_back(s);
     if (failed.empty()) continue;

@@ -67,6 +67,7 @@ EXPORTS = {
     "hkv_ctx_num_devices": (c_int, [c_void_p]),
     "hkv_device_healthy": (c_int, [c_void_p, c_int]),
     "hkv_device_failures": (c_int, [c_void_p, c_int]),
+    "hkv_device_reset_health": (c_int, [c_void_p, c_int]),
     "hkv_debug_fail_device": (c_int, [c_void_p, c_int, c_uint32]),
     "hkv_batch_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "hkv_batch_free": (None, [c_void_p]),

@@ -98,17 +98,23 @@ int hkv_open_devices(const int* device_ids, int n_ids, uint32_t flags, hkv_ctx**
 void hkv_close(hkv_ctx* ctx);
 int hkv_ctx_num_devices(const hkv_ctx* ctx);
 /* Device k of the context still takes host-batch shards (1) or has failed
- * one (0); negative on a bad argument. */
+ * one with a device fault (0); negative on a bad argument. */
 int hkv_device_healthy(hkv_ctx* ctx, int dev);
+/* Give device k host-batch shards again (after the caller has decided it
+ * recovered, e.g. a hipDeviceReset or a passing probe batch). */
+int hkv_device_reset_health(hkv_ctx* ctx, int dev);
 /* Host-batch shards device k has failed (0 or 1: a failed device gets no
  * more shards); negative on a bad argument. */
 int hkv_device_failures(hkv_ctx* ctx, int dev);
 /* Test hook: device k's next host-batch shard fails — HKV_FAIL_ENQUEUE
  * before anything is enqueued, HKV_FAIL_JOIN after its work completed — as a
- * HIP error would, exercising the failover of hkv_verify / hkv_verify_host. */
+ * HIP error would, exercising the failover of hkv_verify / hkv_verify_host;
+ * HKV_FAIL_ALLOC as a staging allocation would (HKV_E_OOM: the call fails,
+ * the device stays healthy). */
 #define HKV_FAIL_NONE 0u
 #define HKV_FAIL_ENQUEUE 1u
 #define HKV_FAIL_JOIN 2u
+#define HKV_FAIL_ALLOC 3u
 int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when);
 
 /* Pinned host record buffer with room for max_n records. */
@@ -119,11 +125,13 @@ size_t hkv_batch_capacity(const hkv_batch* b);
 
 /* Verify records [0, n) of the batch. Shards contiguous 64-aligned index
  * ranges across the context's healthy devices; writes ceil(n/32) words.
- * Blocking. Failover: when a device's shard fails (a HIP error while
- * enqueueing or while waiting for it), that device is marked unhealthy for
- * the rest of the context's life and its shard is re-verified on the devices
- * still healthy; the call fails only when none is left (the last error, or
- * HKV_E_NODEV once every device of the context is unhealthy). */
+ * Blocking. Failover: when a device's shard fails with a device fault (a
+ * HIP error while enqueueing or while waiting for it: HKV_E_HIP), that device
+ * is marked unhealthy until hkv_device_reset_health and its shard is
+ * re-verified on the devices still healthy; the call fails only when none is
+ * left (the last error, or HKV_E_NODEV once every device of the context is
+ * unhealthy). An allocation failure (HKV_E_OOM) is returned as is: no device
+ * changes health and nothing is re-sharded. */
 int hkv_verify(hkv_ctx* ctx, hkv_batch* b, size_t n, uint32_t mode, uint32_t* verdict_bits);
 
 /* Same, from any host memory (copied through the context's staging). */

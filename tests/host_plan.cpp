@@ -125,6 +125,50 @@ int main() {
       std::printf("FAIL: all-fail rc=%d fails=%d\n", rc, fails);
       return 1;
     }
+    // an allocation failure (HKV_E_OOM = -3) on one device ends the call with
+    // that error but takes no device out of service: nothing is re-sharded,
+    // the shards already started are joined, and the next call uses every
+    // device again (one OOM must not cascade over the context)
+    for (int fail_dev = 0; fail_dev < 3; ++fail_dev) {
+      std::vector<bool> h3(3, true);
+      int reported = 0, enq = 0, joins = 0;
+      std::vector<int> in_flight(3, 0);
+      const int rc2 = hkv::run_with_failover(
+          5000, h3,
+          [&](const hkv::Shard& s) {
+            if (s.dev == fail_dev) return -3;
+            ++enq;
+            in_flight[(size_t)s.dev] = 1;
+            return 0;
+          },
+          [&](const hkv::Shard& s) {
+            ++joins;
+            in_flight[(size_t)s.dev] = 0;
+            return 0;
+          },
+          [&](int, int) { ++reported; });
+      if (rc2 != -3 || reported != 0 || !(h3[0] && h3[1] && h3[2]) || joins != enq || in_flight[0] + in_flight[1] + in_flight[2]) {
+        std::printf("FAIL: alloc failure dev=%d rc=%d reported=%d enq=%d joins=%d\n", fail_dev, rc2, reported, enq,
+                    joins);
+        return 1;
+      }
+      int used = 0;
+      if (hkv::run_with_failover(5000, h3, [&](const hkv::Shard&) { ++used; return 0; },
+                                 [](const hkv::Shard&) { return 0; }, [](int, int) {}) != 0 || used != 3) {
+        std::printf("FAIL: devices not reused after an allocation failure\n");
+        return 1;
+      }
+      // the same at join: the error is returned, every started shard joined
+      std::vector<bool> h4(3, true);
+      int joined = 0;
+      const int rc3 = hkv::run_with_failover(
+          5000, h4, [](const hkv::Shard&) { return 0; },
+          [&](const hkv::Shard& s) { ++joined; return s.dev == fail_dev ? -3 : 0; }, [](int, int) {});
+      if (rc3 != -3 || joined != 3 || !(h4[0] && h4[1] && h4[2])) {
+        std::printf("FAIL: alloc failure at join dev=%d rc=%d joined=%d\n", fail_dev, rc3, joined);
+        return 1;
+      }
+    }
     std::vector<bool> none(2, false);
     if (hkv::run_with_failover(10, none, [](const hkv::Shard&) { return 0; }, [](const hkv::Shard&) { return 0; },
                                [](int, int) {}) != -2) {

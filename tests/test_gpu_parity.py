@@ -521,4 +521,16 @@ def test_multi_device_failover_reshards(torch, ver):
         with pytest.raises(HkvError) as e:
             v3.verify_records(host[: 1000 * 168], 1)
         assert e.value.rc == -2                            # HKV_E_NODEV
+        # the caller brings the devices back; an allocation failure (ADVICE
+        # r03: HKV_E_OOM) fails the call but takes no device out of service
+        for k in range(3):
+            assert lib.hkv_device_reset_health(v3.ctx, k) == 0
+        assert lib.hkv_debug_fail_device(v3.ctx, 1, 3) == 0   # HKV_FAIL_ALLOC
+        with pytest.raises(HkvError) as e:
+            v3.verify_records(host, 1)
+        assert e.value.rc == -3                            # HKV_E_OOM
+        assert [lib.hkv_device_healthy(v3.ctx, k) for k in range(3)] == [1, 1, 1]
+        got = v3.verify_records(host, 1)
+        assert (got == single).all()
+        assert [lib.hkv_device_failures(v3.ctx, k) for k in range(3)] == [1, 1, 1]
     assert not single[bad].any() and single.sum() == n - bad.size
