@@ -33,9 +33,11 @@ algorithm's limb products per verify, hkv/opcount.py P_ALG_ECMULT, over the
 HIP-event-timed ecmult + finish launches, against the v_mad_u64_u32 peak at 2.4 GHz and at the
 measured mad rate and clock); configs[0] (the 2,000-tx P2PKH block), [2]
 (block mix) and [3] (adversarial 1M, every class of hkv/adversarial.py); and
-the CPU baseline leg: the C restatement (oracle/, kind "port") and OpenSSL's
-ECDSA_do_verify (the survey's labelled non-reference fallback; libsecp256k1 is
-not installed on the box), single-thread and over a thread sweep (1, 16, 64,
+the CPU baseline leg: a restatement of libsecp256k1's verify algorithm
+(oracle/secp_fast.c: GLV, w = 15 G tables, safegcd — the reference library's
+class), the plain C restatement (oracle/hkv_oracle.c) — both kind "port" — and
+OpenSSL's ECDSA_do_verify (the survey's labelled non-reference fallback;
+libsecp256k1 is not installed on the box), single-thread and over a thread sweep (1, 16, 64,
 128 and the affinity count; the cgroup CPU quota is recorded), on the
 configs[0] block and on config-2 / adversarial samples, with their verdicts
 compared to the GPU's on the same records.
@@ -125,21 +127,29 @@ def cpu_baseline(samples, sweep) -> dict:
     rate of the sweep and `cores` the thread count that reached it. The other
     samples are timed on 1 thread (first 4,096 records) and at that thread
     count; every sample's verdicts are compared with the GPU's.
-    Implementations: "port" = oracle/hkv_oracle.c (C restatement of the
-    reference semantics; no GLV, generic inversions), "openssl" = OpenSSL 3
-    ECDSA_do_verify behind the semantic adapter (oracle/openssl_check.c) —
-    the survey's labelled non-reference fallback, libsecp256k1 being absent."""
+    Implementations: "secpfast" = oracle/secp_fast.c, a restatement of
+    libsecp256k1's verify algorithm (5x52 field, GLV + wNAF5 Strauss, w = 15
+    G tables, variable-time safegcd s^-1: the reference library's class, so
+    north_star's "x the all-core host libsecp256k1 rate" can be judged);
+    "port" = oracle/hkv_oracle.c (C restatement of the reference semantics;
+    no GLV, generic inversions); "openssl" = OpenSSL 3 ECDSA_do_verify behind
+    the semantic adapter (oracle/openssl_check.c) — the survey's labelled
+    non-reference fallback. libsecp256k1 itself is absent on the box."""
     import numpy as np
     import subprocess
     ob = os.path.join(ROOT, "oracle", "build")
-    if not (os.path.exists(os.path.join(ob, "libhkv_oracle.so")) and os.path.exists(os.path.join(ob, "libhkv_openssl.so"))):
+    sos = ("libhkv_oracle.so", "libhkv_openssl.so", "libhkv_secpfast.so")
+    if not all(os.path.exists(os.path.join(ob, x)) for x in sos):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    argt = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     port = ctypes.CDLL(os.path.join(ob, "libhkv_oracle.so"))
-    port.hkvo_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    port.hkvo_verify_batch.argtypes = argt
     ossl = ctypes.CDLL(os.path.join(ob, "libhkv_openssl.so"))
-    ossl.hkvo_openssl_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
-                                               ctypes.c_int]
-    impls = {"port": port.hkvo_verify_batch, "openssl": ossl.hkvo_openssl_verify_batch}
+    ossl.hkvo_openssl_verify_batch.argtypes = argt
+    fast = ctypes.CDLL(os.path.join(ob, "libhkv_secpfast.so"))
+    fast.hkvo_fast_verify_batch.argtypes = argt
+    impls = {"secpfast": fast.hkvo_fast_verify_batch, "port": port.hkvo_verify_batch,
+             "openssl": ossl.hkvo_openssl_verify_batch}
 
     def run(fn, recs, mode, t):
         n = len(recs) // 168
@@ -181,10 +191,15 @@ def cpu_baseline(samples, sweep) -> dict:
     return {"value": round(rate, 1) if first else None, "unit": "verifies/s", "cores": cores,
             "kind": "port",
             "impl": impl,
+            "impl_note": {"secpfast": "oracle/secp_fast.c: libsecp256k1's verify algorithm restated (5x52 field, "
+                                      "GLV + wNAF5, w=15 G tables, safegcd), incl. the pubkey parse / sqrt",
+                          "port": "oracle/hkv_oracle.c: plain restatement (no GLV, Fermat inversions)",
+                          "openssl": "OpenSSL 3 ECDSA_do_verify behind oracle/openssl_check.c"},
             "sample": f"BASELINE configs[0]: the 4,000 inputs of the 2,000-tx P2PKH block (records extracted on "
-                      f"device, HKV_HASKOIN = verifyHashSig), tiled to 1,500 records per thread; best of the C "
-                      f"restatement (port) and OpenSSL ECDSA_do_verify over the thread sweep {list(sweep)} "
-                      f"(value at cores = {cores} threads); libsecp256k1 is not installed on the box",
+                      f"device, HKV_HASKOIN = verifyHashSig), tiled to 1,500 records per thread; best of the "
+                      f"libsecp256k1-class restatement (secpfast), the plain C restatement (port) and OpenSSL "
+                      f"ECDSA_do_verify over the thread sweep {list(sweep)} (value at cores = {cores} threads); "
+                      f"libsecp256k1 itself is not installed on the box",
             "thread_sweep": list(sweep),
             "single_thread_value": res.get(first, {}).get(impl, {}).get("1_thread") if first else None,
             "samples": res, "host": host_info()}
@@ -773,6 +788,15 @@ def main() -> None:
                     samples.append((f"config3_sample_{'libsecp' if mode == 0 else 'haskoin'}",
                                     adv_recs[: m4 * 168], mode, adv_got[mode][:m4]))
             cpu = cpu_baseline(samples, thread_sweep())
+            # north_star: ">= 50x the all-core host libsecp256k1 verify rate"
+            # (here: the job's CPU share, see cpu_baseline.host.cgroup)
+            if cpu.get("value"):
+                cpu["gpu_over_cpu"] = {
+                    "all_core": round(value / cpu["value"], 1),
+                    "single_thread": round(value / cpu["single_thread_value"], 1)
+                    if cpu.get("single_thread_value") else None,
+                    "note": "value (configs[1], HBM-resident) / the best CPU rate of the sweep (impl, cores); the "
+                            "CPU figure is the job's cgroup CPU share, not the whole host"}
             if c0_recs is not None:
                 cpu["config0_host_sighash"] = cpu_sighash_leg(c0_txs, c0_inputs, c0_recs)
         if config4:

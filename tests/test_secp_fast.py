@@ -1,0 +1,134 @@
+"""The libsecp256k1-class CPU stand-in (oracle/secp_fast.c, bench.py's
+cpu_baseline fast leg) against the port (oracle/hkv_oracle.c) and the
+fixtures (CPU only):
+
+- every golden KAT class and the special pool (r + n branch, edge scalars,
+  u1 = 0, msg >= n, sum = infinity, ladder collisions), both modes, equal to
+  the manifest labels;
+- every adversarial class of hkv.adversarial (configs[3]) and generated
+  configs[4]-style batches (5-30% invalid), equal to the port and the labels;
+- its s^-1 (variable-time safegcd) against pow(s, -1, n) on edge and random
+  scalars, and its GLV split: k1 + k2 lambda == k (mod n), |k1|, |k2| < 2^129;
+- it is the faster checker: >= 3x the port's single-thread rate."""
+import ctypes
+import json
+import os
+import random
+import time
+
+import numpy as np
+import pytest
+
+import secp256k1_oracle as o
+from conftest import GOLDEN, ROOT, c_gen_batch, oracle_batch
+from hkv import adversarial
+
+FAST_SO = os.path.join(ROOT, "oracle", "build", "libhkv_secpfast.so")
+
+
+@pytest.fixture(scope="module")
+def fast():
+    if not os.path.exists(FAST_SO):
+        import subprocess
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    lib = ctypes.CDLL(FAST_SO)
+    lib.hkvo_fast_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_int]
+    lib.hkvo_fast_sc_inverse.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.hkvo_fast_glv_split.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]
+    return lib
+
+
+def fast_batch(lib, recs, mode, threads=8):
+    recs = np.ascontiguousarray(np.frombuffer(bytes(recs), dtype=np.uint8) if isinstance(recs, bytes) else recs)
+    n = len(recs) // 168
+    out = np.zeros(n, dtype=np.uint8)
+    lib.hkvo_fast_verify_batch(recs.ctypes.data, n, mode, out.ctypes.data, threads)
+    return out.astype(bool)
+
+
+@pytest.mark.parametrize("mode,key", [(0, "libsecp"), (1, "haskoin")])
+def test_golden_kats_and_special_pool(fast, mode, key):
+    man = json.load(open(os.path.join(GOLDEN, "kat_manifest.json")))
+    data = open(os.path.join(GOLDEN, "kat_records.bin"), "rb").read()
+    got = fast_batch(fast, data, mode)
+    exp = np.array([r[key] for r in man["records"]])
+    bad = [man["records"][i]["class"] for i in np.nonzero(got != exp)[0]]
+    assert not bad, bad
+    sp = json.load(open(os.path.join(GOLDEN, "special_pool.json")))
+    data = open(os.path.join(GOLDEN, "special_pool.bin"), "rb").read()
+    got = fast_batch(fast, data, mode)
+    exp = np.array([r[key] for r in sp["records"]])
+    bad = sorted({sp["records"][i]["class"] for i in np.nonzero(got != exp)[0]})
+    assert not bad, bad
+
+
+def test_every_adversarial_class(fast, coracle):
+    rng = random.Random(11)
+    recs = []
+    for i in range(64):
+        q = o.point_mul(rng.randrange(1, o.N), o.G)
+        m, r, s = o.keyless_tuple(rng.randrange(1, o.N), rng.randrange(1, o.N), q)
+        if s > o.N // 2:
+            s = o.N - s
+        recs.append(o.make_record(m, r.to_bytes(32, "big") + s.to_bytes(32, "big"), o.pubkey_serialize(q, i % 5 != 0)))
+    base = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    adv, lib_lab, hask_lab, cls = adversarial.mutate(np.tile(base, 30), seed=17, invalid_frac=0.7, special_frac=0.2)
+    for mode, lab in ((0, lib_lab), (1, hask_lab)):
+        got = fast_batch(fast, adv, mode)
+        assert (got == oracle_batch(coracle, adv.tobytes(), mode)).all()
+        bad = sorted({adversarial.CLASSES[c] for c in cls[got != lab]})
+        assert not bad, (mode, bad)
+
+
+@pytest.mark.parametrize("seed,inv", [(0x484B5635, 50), (0x1234, 300)])
+def test_generated_batches_equal_port(fast, coracle, seed, inv):
+    recs, lab, _ = c_gen_batch(coracle, seed, 4096, 2000, 64, 100, inv)
+    for mode in (0, 1):
+        got = fast_batch(fast, recs, mode)
+        assert (got == oracle_batch(coracle, recs.tobytes(), mode)).all()
+        assert (got == lab).all()
+
+
+def test_scalar_inverse(fast):
+    rng = random.Random(5)
+    vals = [1, 2, 3, o.N - 1, o.N - 2, o.N // 2, 2**128, 2**255 % o.N, (1 << 62) - 1, 1 << 62, 1 << 124]
+    vals += [rng.randrange(1, o.N) for _ in range(3000)]
+    out = ctypes.create_string_buffer(32)
+    for v in vals:
+        fast.hkvo_fast_sc_inverse(v.to_bytes(32, "big"), out)
+        assert int.from_bytes(out.raw, "big") == pow(v, -1, o.N), hex(v)
+
+
+def test_glv_split(fast):
+    lam = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+    rng = random.Random(6)
+    vals = [0, 1, o.N - 1, lam, o.N - lam, (o.N - 1) // 2] + [rng.randrange(o.N) for _ in range(3000)]
+    m1 = (ctypes.c_uint64 * 3)()
+    m2 = (ctypes.c_uint64 * 3)()
+    s1, s2 = ctypes.c_int(), ctypes.c_int()
+    for k in vals:
+        fast.hkvo_fast_glv_split(k.to_bytes(32, "big"), m1, ctypes.byref(s1), m2, ctypes.byref(s2))
+        a = m1[0] | m1[1] << 64 | m1[2] << 128
+        b = m2[0] | m2[1] << 64 | m2[2] << 128
+        assert a < 2**129 and b < 2**129
+        assert (s1.value * a + s2.value * b * lam - k) % o.N == 0
+
+
+def test_faster_than_port(fast, coracle):
+    """The point of the stand-in: of the reference library's class (GLV,
+    w = 15 G tables, safegcd), >= 3x the port's rate on one thread."""
+    recs, _, _ = c_gen_batch(coracle, 0x484B5632, 0, 1200, 64, 100, 0)
+
+    def rate(fn):
+        out = np.zeros(1200, dtype=np.uint8)
+        best = 0.0
+        for _ in range(2):
+            t0 = time.perf_counter()
+            fn(recs.ctypes.data_as(ctypes.c_void_p), 1200, 0, out.ctypes.data_as(ctypes.c_void_p), 1)
+            best = max(best, 1200 / (time.perf_counter() - t0))
+        assert out.all()
+        return best
+
+    assert rate(fast.hkvo_fast_verify_batch) >= 3 * rate(coracle.hkvo_verify_batch)
