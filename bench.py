@@ -233,6 +233,30 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
         torch.cuda.synchronize()
         res[f"{name}_us"] = round(e0.elapsed_time(e1) * 1e3 / k, 1)
     res["inputs_per_s"] = round(db.n / (res["total_us"] * 1e-6), 1)
+    # one block at a time (the stream idle before each call): its latency
+    lat = []
+    for _ in range(max(3, k // 2)):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(bstream)
+        run()
+        e1.record(bstream)
+        torch.cuda.synchronize()
+        lat.append(e0.elapsed_time(e1) * 1e3)
+    res["latency_us"] = round(sorted(lat)[len(lat) // 2], 1)
+    # 32 blocks enqueued back to back (the device entry point only enqueues:
+    # the host's clock runs from the first enqueue to the last verdict)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(32):
+        run()
+    t_enq = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t32 = time.perf_counter() - t0
+    res["back_to_back32"] = {"blocks_per_s": round(32 / t32, 1), "us_per_block": round(t32 / 32 * 1e6, 1),
+                             "enqueue_us_per_block": round(t_enq / 32 * 1e6, 1),
+                             "note": "32 calls of hkv_verify_std_inputs_device on one stream, no host sync between "
+                                     "them; host wall clock from the first enqueue to the last verdict"}
     res["split_phases_us"] = split_phases(v, torch, run)
     return res, got
 

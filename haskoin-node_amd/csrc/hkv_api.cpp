@@ -8,14 +8,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/hkv.h"
@@ -52,15 +50,13 @@ struct DevCtx {
   // [0..3] tx batch, [4] sighash out, [5] header batch, [6] spare
   void* stage[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t stage_cap[7] = {0, 0, 0, 0, 0, 0, 0};
-  // multisig inputs (hkv_sighash.hip section 4): [0] desc words, [1] record
-  // totals (device), [2] offsets, [4] candidate + key records, [5] key bits,
-  // [6] host-form verdict words
+  // multisig inputs (hkv_sighash.hip section 4, hkv_kernels.hip 2e): [0] desc
+  // words, [2] offsets, [3] candidate verdict words, [4] candidate + key
+  // records, [5] key-check verdict words, [6] host-form verdict words
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t* ms_total = nullptr;  // pinned: [0] sum (candidates | keys << 32), [1] sequence number
-  uint64_t ms_seq = 0;           // last sequence number handed to hkv_ms_scan_kernel
-  uint64_t* ms_total_dev = nullptr;  // its device-side address
-  void* ms_ctr = nullptr;            // device counters of hkv_ms_scan_kernel
+  void* ms_ctr = nullptr;            // scan counters: [0] running sum, [1] finished groups, [2] published total
+  unsigned int* ms_bar = nullptr;    // the tail kernel's grid barrier: [0] arrivals, [1] sense, [2] fault
   bool ms_dirty = false;             // a call failed after its scan launch: zero ms_ctr before the next scan
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
   bool rare_dirty = false;           // a finish launch failed part-way: zero rare_ctr before the next one
@@ -87,9 +83,8 @@ struct hkv_ctx {
   // mu: every entry point's host-side state (DevCtx fields, allocations,
   // enqueue order). tx_mu[k]: the tx-index rows, the multisig scratch and
   // the tx staging of device k — held by the sighash / std-input entry
-  // points for their whole call, taken BEFORE mu. hkv_verify_std_inputs_device
-  // releases mu (never tx_mu) while it waits for its multisig count, so the
-  // other entry points keep running on the device meanwhile.
+  // points for their whole call, taken BEFORE mu. No entry point waits on
+  // the device while it holds either (the device forms only enqueue).
   std::mutex mu;
   std::vector<std::unique_ptr<std::mutex>> tx_mu;
   // host-batch failover (verify_from_host): devices still in use, and how
@@ -128,9 +123,13 @@ size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 #define HKV_SPLIT_DIV 8
 #endif
 
-// verify-std-inputs batches: the scan kernel sums candidates (<= 136 per
-// 16-of-16 input) in the low 32 bits of one 64-bit device counter
-constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFFFFull / 136;
+// verify-std-inputs batches run in chunks of at most STD_CHUNK inputs: the
+// multisig scratch of a chunk is sized by its host bound (136 candidate and
+// 16 key-check records per input: 16-of-16), so the device never reports a
+// count the host must read first; the scan's 32-bit candidate sum cannot wrap
+constexpr size_t STD_CHUNK = 1u << 17;
+constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
+constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFF00ull;
 
 int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
   if (d.im_cap < n_pad) {
@@ -254,15 +253,12 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
   HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
   HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
-  // fine-grained and mapped: hkv_ms_scan_kernel stores the multisig sum here
-  HKV_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.ms_total), 2 * sizeof(uint64_t),
-                        hipHostMallocCoherent | hipHostMallocMapped),
-          "hipHostMalloc(multisig)");
-  HKV_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d.ms_total_dev), d.ms_total, 0),
-          "hipHostGetDevicePointer(multisig)");
-  // total + finished-workgroup count; the scan kernel re-arms them itself
-  HKV_TRY(hipMalloc(&d.ms_ctr, 2 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
-  HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
+  // running sum + finished-workgroup count (the scan re-arms them itself) +
+  // the published total the multisig tail reads; the tail's barrier words
+  HKV_TRY(hipMalloc(&d.ms_ctr, 4 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
+  HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 4 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
+  HKV_TRY(hipMalloc(reinterpret_cast<void**>(&d.ms_bar), 4 * sizeof(unsigned int)), "hipMalloc(multisig barrier)");
+  HKV_TRY(hipMemsetAsync(d.ms_bar, 0, 4 * sizeof(unsigned int), d.stream), "hipMemset(multisig barrier)");
   HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
@@ -303,8 +299,8 @@ void free_device(DevCtx& d) {
     if (p) (void)hipFree(p);
   for (auto p : d.ms)
     if (p) (void)hipFree(p);
-  if (d.ms_total) (void)hipHostFree(d.ms_total);
   if (d.ms_ctr) (void)hipFree(d.ms_ctr);
+  if (d.ms_bar) (void)hipFree(d.ms_bar);
   if (d.rare_ctr) (void)hipFree(d.rare_ctr);
   if (d.aux) (void)hipFree(d.aux);
   if (d.hbits) (void)hipHostFree(d.hbits);
@@ -398,40 +394,6 @@ int enqueue_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, 
   return HKV_OK;
 }
 
-// Wait until hkv_ms_scan_kernel has published sequence number seq (its last
-// workgroup stores the sum, then seq, into the pinned words). Yields on every
-// iteration and sleeps once the wait is long; a launch that failed never
-// publishes, so every 256 iterations the stream's state is checked.
-int wait_ms_total(DevCtx& d, hipStream_t st, uint64_t seq, uint64_t* total) {
-  volatile uint64_t* hv = d.ms_total;
-  for (uint32_t spin = 1; hv[1] != seq; ++spin) {
-    if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    else std::this_thread::yield();
-    if ((spin & 255u) == 0) {
-      const hipError_t q = hipStreamQuery(st);
-      if (q == hipErrorNotReady) continue;
-      if (hv[1] == seq) break;
-      if (q != hipSuccess) return hip_fail(q, "multisig scan");
-      g_last_hip = "multisig scan finished without publishing its sum";
-      return HKV_E_INTERNAL;
-    }
-  }
-  *total = hv[0];
-  return HKV_OK;
-}
-
-// Full verifyStdInput over a job batch, verdict bit i -> out_bits (device).
-// Single-signature templates: one record per input (recs) through the verify
-// kernels. Multisig (bare / P2SH / P2WSH): the scan kernel's candidate counts
-// are summed on device and published to a pinned host word; the host reads
-// that sum (the one wait of the device form, overlapped with the main verify
-// already enqueued behind the scan) and, when there are any multisig inputs,
-// enqueues the verify of their candidate and key-check records and
-// hkv_ms_resolve_kernel, which ORs their verdicts into out_bits.
-// lk (the context lock, held by the caller; may be null): released while the
-// host waits for the sum, after publishing this call's scratch use, and
-// re-taken before the multisig work is enqueued (the caller also holds the
-// device's tx lock, which guards txt and the multisig scratch across the gap).
 // Small batches of standard inputs in one verify launch (hkv_pair_split_kernel
 // <true>): the chains start from the parsed keys and signatures while the
 // signature wave computes the sighashes and script checks beside them.
@@ -459,78 +421,92 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
   return HKV_OK;
 }
 
-int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
-                              void* recs, uint32_t* out_bits, hipStream_t st,
-                              std::unique_lock<std::mutex>* lk = nullptr) {
-  // small batches: tx index, then one fused launch (the multisig scan after
-  // it, off the block's critical path); larger ones: the extraction kernel,
-  // then the record verify
+// Full verifyStdInput over a chunk of at most STD_CHUNK jobs, verdict bit i
+// -> out_bits (device), all enqueued on st (nothing waits on the host).
+// Single-signature templates: one record per input (recs) through the verify
+// kernels — small batches in one fused launch (tx index, then the block or
+// pair kernel with the parse, the hashes and the script checks inside),
+// larger ones the extraction kernel then the record verify. Multisig (bare /
+// P2SH / P2WSH / P2SH-P2WSH): the scan (inside the block kernel, or
+// hkv_ms_scan_kernel) leaves the batch total on the device and the tail
+// kernel (hkv_kernels.hip 2e) does the rest, or nothing when the total is 0.
+int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
+                      uint32_t* out_bits, hipStream_t st) {
   const bool fused = split_batch(d, n);
   // the block kernel (at most 16 inputs per CU) runs the multisig scan on
-  // its square-root wave; otherwise the scan kernel follows the verify launch
+  // its signature wave; otherwise the scan kernel follows the verify launch
   const bool fused_scan = fused && hkv::std_split_scans((uint32_t)round_up(n, hkv::WG), (uint32_t)d.n_cu);
+  const size_t cap_cand = n * MS_CAND_PER_INPUT, cap_keys = n * MS_KEYS_PER_INPUT;
+  const size_t slots = hkv::ms_tail_slots((uint32_t)d.n_cu);
   int rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
   if (!rc) rc = grow(&d.ms[2], &d.ms_cap[2], n * 8, "hipMalloc(multisig offsets)");
+  if (!rc) rc = grow(&d.ms[3], &d.ms_cap[3], round_up(cap_cand, 64) / 8, "hipMalloc(multisig candidate bits)");
+  if (!rc) rc = grow(&d.ms[4], &d.ms_cap[4], (cap_cand + cap_keys) * hkv::REC_SIZE, "hipMalloc(multisig records)");
+  if (!rc) rc = grow(&d.ms[5], &d.ms_cap[5], round_up(cap_keys, 64) / 8, "hipMalloc(multisig key bits)");
+  // the tail's candidate groups use slot-relative pair-form scratch (grid * 32 signatures)
+  if (!rc) rc = ensure_dev_buffers(d, std::max(round_up(n, hkv::WG), round_up(slots, hkv::WG)));
+  if (!rc) rc = ensure_aux(d, std::max(round_up(n, hkv::WG), round_up(slots, hkv::WG)), st);
   if (rc) return rc;
   uint32_t* desc = static_cast<uint32_t*>(d.ms[0]);
   uint64_t* off = static_cast<uint64_t*>(d.ms[2]);
-  // (an event record here instead of the pinned word would put a barrier
-  // packet between the scan and the verify, ~5 us on the block path)
-  const uint64_t seq = ++d.ms_seq;
   if (d.ms_dirty) {  // an earlier call failed after its scan launch: counters may be stale
-    HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), st), "hipMemset(multisig counters)");
+    HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 3 * sizeof(uint64_t), st), "hipMemset(multisig counters)");
     d.ms_dirty = false;
   }
-  d.ms_dirty = true;  // until this call has read the sum
-  const hkv::MsScan ms{desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq};
+  d.ms_dirty = true;  // until this call's tail is enqueued
+  uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr);
+  const hkv::MsScan ms{desc, off, ctr};
   rc = fused ? enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, fused_scan ? &ms : nullptr, st);
   if (rc) return rc;
   if (!fused_scan)
     HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
-                                desc, off, static_cast<uint64_t*>(d.ms_ctr), d.ms_total_dev, seq, st),
+                                desc, off, ctr, st),
             "multisig scan launch");
   if (!fused) {
     rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
     if (rc) return rc;
   }
-  uint64_t total = 0;
-  if (lk) {
-    rc = scratch_release(d, st);
-    if (rc) return rc;
-    lk->unlock();
-    rc = wait_ms_total(d, st, seq, &total);
-    lk->lock();
-    if (rc) return rc;
-    HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
-    rc = scratch_acquire(d, st);
-    if (rc) return rc;
-  } else {
-    rc = wait_ms_total(d, st, seq, &total);
-    if (rc) return rc;
-  }
-  d.ms_dirty = false;
-  const size_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
-  if (n_keys == 0) return HKV_OK;  // no multisig input
-  rc = grow(&d.ms[4], &d.ms_cap[4], (n_cand + n_keys) * hkv::REC_SIZE, "hipMalloc(multisig records)");
-  if (!rc) rc = grow(&d.ms[5], &d.ms_cap[5], round_up(n_keys, hkv::WG) / 8, "hipMalloc(multisig key bits)");
-  if (rc) return rc;
   uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
-  uint8_t* keyrec = cand + n_cand * hkv::REC_SIZE;
-  uint32_t* kbits = static_cast<uint32_t*>(d.ms[5]);
-  if (fused) {  // the multisig sighashes read the BIP143 per-tx hashes from the index rows
-    rc = enqueue_tx_index(d, dt, st, std_tx_hashes(forkid));
+  hkv::MsTail t;
+  t.txs = dt->bytes;
+  t.tx_off = dt->offsets;
+  t.n_tx = dt->n_tx;
+  t.txt = d.txt;
+  t.scripts = dt->scripts;
+  t.scripts_len = dt->scripts_len;
+  t.jobs = jobs;
+  t.n = (uint32_t)n;
+  t.forkid = forkid;
+  // the fused launch's index hashed nothing: the multisig sighashes need the
+  // BIP143 per-tx hashes the network allows (the extraction path built them)
+  t.hash_txs = fused ? std_tx_hashes(forkid) : hkv::TX_HASHES_NONE;
+  t.desc = desc;
+  t.off = off;
+  t.total = reinterpret_cast<const unsigned long long*>(ctr + 2);
+  t.cand = cand;
+  t.keyrec = cand + cap_cand * hkv::REC_SIZE;
+  t.cbits = static_cast<uint32_t*>(d.ms[3]);
+  t.kbits = static_cast<uint32_t*>(d.ms[5]);
+  t.im = d.im;
+  t.aux = d.aux;
+  t.gtab = d.gtab;
+  t.qs = d.qs;
+  t.out_bits = out_bits;
+  t.bar = d.ms_bar;
+  HKV_TRY(hkv::launch_ms_tail(t, (uint32_t)d.n_cu, st), "multisig tail launch");
+  d.ms_dirty = false;
+  return HKV_OK;
+}
+
+int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                              void* recs, uint32_t* out_bits, hipStream_t st) {
+  for (size_t lo = 0; lo < n; lo += STD_CHUNK) {
+    const size_t cn = std::min(STD_CHUNK, n - lo);
+    const int rc = enqueue_std_chunk(d, dt, jobs + lo, cn, forkid, static_cast<uint8_t*>(recs) + lo * hkv::REC_SIZE,
+                                     out_bits + lo / 32, st);
     if (rc) return rc;
   }
-  HKV_TRY(hkv::launch_ms_emit(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
-                              desc, off, cand, keyrec, st),
-          "multisig emit launch");
-  HKV_TRY(hkv::launch_pubkey_check(keyrec, (uint32_t)n_keys, kbits, st), "pubkey check launch");
-  if (n_cand) {
-    rc = enqueue_verify(d, cand, n_cand, HKV_MODE_HASKOIN, st);
-    if (rc) return rc;
-  }
-  HKV_TRY(hkv::launch_ms_resolve(desc, off, (uint32_t)n, d.bits, kbits, out_bits, st), "multisig resolve launch");
   return HKV_OK;
 }
 
@@ -993,12 +969,12 @@ int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, co
   if (n == 0) return HKV_OK;
   if (!d_jobs || !d_records || !d_bits) return HKV_E_ARG;
   std::lock_guard<std::mutex> txl(*ctx->tx_mu[dev]);
-  std::unique_lock<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::mutex> lock(ctx->mu);
   DevCtx& d = ctx->devs[dev];
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = scratch_acquire(d, st);
-  if (!rc) rc = enqueue_verify_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, d_bits, st, &lock);
+  if (!rc) rc = enqueue_verify_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, d_bits, st);
   if (rc) return rc;
   return scratch_release(d, st);
 }
@@ -1029,7 +1005,15 @@ int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job*
                                    static_cast<uint32_t*>(d.ms[6]), d.stream);
   if (rc) return rc;
   HKV_TRY(hipMemcpyAsync(verdict_bits, d.ms[6], (n + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
+  unsigned int fault = 0;
+  HKV_TRY(hipMemcpyAsync(&fault, d.ms_bar + 2, sizeof(fault), hipMemcpyDeviceToHost, d.stream), "D2H tail fault");
   HKV_TRY(hipStreamSynchronize(d.stream), "std inputs sync");
+  if (fault) {  // the multisig tail's grid barrier gave up (its verdicts stayed 0): report it once
+    HKV_TRY(hipMemsetAsync(d.ms_bar + 2, 0, sizeof(unsigned int), d.stream), "hipMemset(tail fault)");
+    g_last_hip = "multisig tail: grid barrier timed out (workgroups not co-resident)";
+    (void)scratch_release(d, d.stream);
+    return HKV_E_INTERNAL;
+  }
   return scratch_release(d, d.stream);
 }
 

@@ -32,14 +32,45 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          unsigned long long* clk, uint32_t* aux, const void* recs, uint32_t mode, uint32_t n_cu,
                          hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
-// the multisig scan operands a fused launch may take over (hkv_ms_scan_kernel's)
+// the multisig scan operands a fused launch may take over (hkv_ms_scan_kernel's);
+// counters: [0] running sum, [1] finished groups, [2] the published total
 struct MsScan {
   uint32_t* desc;
   uint64_t* off;
   uint64_t* counters;
-  uint64_t* host_total;
-  uint64_t seq;
 };
+// The multisig tail (hkv_kernels.hip hkv_ms_tail_kernel): one launch after the
+// scan that does nothing when the batch has no multisig input and otherwise
+// the BIP143 per-tx hashes (hash_txs), the candidate / key-check records, the
+// key checks, the candidate verifies and the countMulSig walk — read from the
+// device total, so the host never waits for it.
+struct MsTail {
+  const uint8_t* txs;
+  const uint32_t* tx_off;
+  uint32_t n_tx;
+  uint32_t* txt;
+  const uint8_t* scripts;
+  uint32_t scripts_len;
+  const hkv_input_job* jobs;
+  uint32_t n;
+  int32_t forkid;
+  uint32_t hash_txs;  // TX_HASHES_* the tail computes first (the fused path's index hashed nothing)
+  const uint32_t* desc;
+  const uint64_t* off;
+  const unsigned long long* total;  // MsScan counters + 2
+  uint8_t* cand;                    // candidate records (capacity n * 136)
+  uint8_t* keyrec;                  // key-check records (capacity n * 16)
+  uint32_t* cbits;                  // candidate verdict words
+  uint32_t* kbits;                  // key-check verdict words
+  uint32_t* im;                     // pair-form scratch: slot stride = grid * 32
+  uint32_t* aux;
+  const uint32_t* gtab;
+  uint32_t* qs;
+  uint32_t* out_bits;               // the batch's verdict words (multisig inputs are ORed in)
+  unsigned int* bar;                // grid barrier words [count, sense]
+};
+hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st);
+uint32_t ms_tail_slots(uint32_t n_cu);  // signatures in flight (im / aux slots the tail needs)
 // small batches of standard inputs in one launch; with ms, the block kernel
 // (std_split_scans) also runs the multisig scan
 hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
@@ -70,17 +101,10 @@ hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt
 hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                              uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                              uint8_t* recs, hipStream_t st);
-// multisig inputs (hkv_sighash.hip section 4; pubkey check in hkv_kernels.hip)
+// multisig inputs: the scan (hkv_sighash.hip section 4; the tail in hkv_kernels.hip)
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
-                          uint32_t* desc, uint64_t* off, uint64_t* counters, uint64_t* host_total, uint64_t seq,
-                          hipStream_t st);
-hipError_t launch_ms_emit(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                          uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
-                          const uint32_t* desc, const uint64_t* off, uint8_t* cand, uint8_t* keyrec, hipStream_t st);
-hipError_t launch_ms_resolve(const uint32_t* desc, const uint64_t* off, uint32_t n, const uint32_t* cbits,
-                             const uint32_t* kbits, uint32_t* out_bits, hipStream_t st);
-hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st);
+                          uint32_t* desc, uint64_t* off, uint64_t* counters, hipStream_t st);
 // hkv_headers.hip
 hipError_t launch_headers(const uint8_t* hdrs, uint32_t n, const uint8_t* pow_limit, const uint8_t* prev0,
                           uint8_t* hashes, uint8_t* status, hipStream_t st);

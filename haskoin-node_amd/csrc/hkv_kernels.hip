@@ -193,10 +193,8 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(co
 // Key-only check (the keys of a CHECKMULTISIG script: haskoin-core decodes
 // every key with importPubKey, so one key off the curve fails the input
 // whatever its signatures do): bit i = record i's key parses. Bits leave as
-// one 64-bit ballot word per wave, like the verify kernel's.
-__global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_pubkey_check_kernel(const uint32_t* __restrict__ recs,
-                                                                                uint32_t n, uint32_t* __restrict__ bits) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+// one 64-bit ballot word per wave (i's wave covers 64 consecutive records).
+HKV_DEV void key_check_lane(const uint32_t* __restrict__ recs, uint32_t i, uint32_t n, uint32_t* __restrict__ bits) {
   uint32_t w[REC_WORDS];
 #pragma unroll
   for (int k = 0; k < REC_WORDS; ++k) w[k] = 0;
@@ -207,8 +205,8 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_pubkey_check_kerne
   fe x, y;
   const bool ok = pubkey_parse_rec(w, x, y) && i < n;
   const uint64_t ball = __ballot(ok);
-  if ((threadIdx.x & 63) == 0) {
-    const uint32_t wbase = i & ~63u;
+  const uint32_t wbase = i & ~63u;
+  if ((threadIdx.x & 63) == 0 && wbase < n) {  // (a wave wholly past n writes nothing)
     bits[wbase / 32] = (uint32_t)ball;
     bits[wbase / 32 + 1] = (uint32_t)(ball >> 32);
   }
@@ -694,8 +692,6 @@ struct StdArgs {
   uint32_t* ms_desc;
   uint64_t* ms_off;
   unsigned long long* ms_ctr;
-  volatile unsigned long long* ms_host;
-  unsigned long long ms_seq;
 };
 
 // Pair-form pieces shared by the small-batch kernels (2c, 2d). Each chain
@@ -990,11 +986,121 @@ HKV_DEV void join_inputs(const uint32_t* __restrict__ im, const uint32_t* __rest
   is_sq = aux[(size_t)AUX_SQ * n_pad + i] != 0;
 }
 
+// One group of PAIR_SIGS signatures (records base .. base + 31) on the
+// workgroup's four waves: the body of hkv_pair_split_kernel, shared with the
+// multisig tail kernel (which passes slot-relative im / aux and shifted
+// record / verdict pointers, so its scratch is sized by the grid, not the batch).
+template <bool STD>
+HKV_DEV void pair_group(uint32_t base, uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
+                        const uint32_t* __restrict__ gtab, uint32_t* __restrict__ bits, uint32_t n_words,
+                        uint32_t* __restrict__ aux, uint32_t* __restrict__ recs, uint32_t mode,
+                        unsigned long long* __restrict__ clk, const StdArgs& sa, QLane* qlds, HLane* hlds,
+                        uint32_t* xch, uint32_t* shabuf) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ln = threadIdx.x & 63;
+  const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
+  const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
+  auto mark = [&](int slot) {
+    if (stamp) clk[4 + slot] = wall_clock64();
+  };
+  if (wv == 2) {
+    // ---- the signature: u2 half (lanes 0-31), then the u1 half and A = u1 G ----
+    const uint32_t i = base + ln;
+    const bool on = ln < PAIR_SIGS;
+    uint32_t flags;
+    bool use;
+    sc sinv, m;
+    StdIn x = {};
+    sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags);
+    __threadfence_block();
+    mark(STAMP_SIG);
+    __syncthreads();  // barrier P
+    sig_wave_gsum<STD>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
+    __threadfence_block();
+    mark(STAMP_GSUM);
+    __syncthreads();  // barrier A
+    __syncthreads();  // barrier B
+    return;
+  }
+  if (wv == 3) {
+    // ---- the key's y0 = sqrt(w) with the key's y parity (lanes 0-31) ----
+    __syncthreads();  // barrier P (nothing to wait for: the key bytes are input)
+    if (ln < PAIR_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
+    __threadfence_block();
+    mark(STAMP_SQRT);
+    __syncthreads();  // barrier A
+    __syncthreads();  // barrier B
+    return;
+  }
+
+  // ---- chain waves: half = wv (0: k1 * Q', 1: k2 * lambda(Q')) ----
+  const int half = wv;
+  const uint32_t c = ln >> 1;                    // signature of the pair
+  const uint32_t i = base + c;
+  ge q;
+  key_point<STD>(i, n, recs, sa, q);
+  // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
+  fe Zg, Qxy;
+  fe_sel(Qxy, q.x, q.y, odd);
+  pair_table(Qxy, half, odd, qlds[half], hlds[half], ln, Zg);
+  mark(half ? STAMP_TABLE1 : STAMP_TABLE0);
+  __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
+  if (half == 0) mark(STAMP_P);
+  const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
+  const bool valid = (i < n) && (flags & FLAG_VALID);
+  const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
+
+  // ---- the chain: 33 radix-16 windows, pair form ----
+  fe P, Z;
+  bool inf;
+  pair_chain(P, Z, inf, qlds[half], im, n_pad, i, valid, negh, half, odd, ln, NWIN - 1, 0);
+
+  mark(half ? STAMP_CHAIN1 : STAMP_CHAIN0);
+  // ---- join: half 1's sum to half 0 through LDS ----
+  if (half == 1) pair_publish(xch, PAIR_SIGS, c, P, Z, inf, odd);
+  fe Y, Zx;
+  fe_xch(Y, P);   // even lane: Y of the pair
+  fe_xch(Zx, Z);  // even lane: Z of the pair
+  __syncthreads();  // barrier A: half 1's sum, A and y0 are published
+  if (half == 0) mark(STAMP_A);
+  bool accept = false;
+  if (half == 0) {  // both lanes compute; the even lane's result is the verdict
+    gej acc, b;
+    acc.x = P;
+    acc.y = Y;
+    acc.z = Zx;
+    bool binf;
+    xch_read(xch, PAIR_SIGS, c, b, binf);
+    gej_add_var(acc, inf, b, binf);  // B' = u2 Q' on E_w (iso scale Zg)
+    gej A;
+    fe y0;
+    uint32_t r[8], af;
+    bool is_sq;
+    join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
+    // B = phi^-1(B') = (X, Y, Z Zg y0) on E, R = A + B exactly, x compare
+    gej bb;
+    bb.x = acc.x;
+    bb.y = acc.y;
+    fe zt;
+    fe_mul(zt, acc.z, Zg);
+    fe_mul(bb.z, zt, y0);
+    bool rinf = (af & AUXF_AINF) != 0;
+    gej_add_var(A, rinf, bb, inf);
+    accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r) && (!STD || (af & AUXF_STDOK));
+  }
+  const uint64_t ball = __ballot(accept && !odd);
+  if (half == 0) mark(STAMP_JOIN);
+  if (half == 0 && ln == 0) {
+    const uint32_t wi = base / 32;
+    if (wi < n_words) bits[wi] = even_bits(ball);
+  }
+  __syncthreads();  // barrier B: the next group's writers of xch / aux wait for the readers
+}
+
 template <bool STD>
 __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* __restrict__ im, uint32_t n,
                                                                      uint32_t n_pad,
                                                                      const uint32_t* __restrict__ gtab,
-                                                                     uint32_t* __restrict__ qs,
                                                                      uint32_t* __restrict__ bits, uint32_t n_words,
                                                                      uint32_t* __restrict__ aux,
                                                                      uint32_t* __restrict__ recs,
@@ -1007,111 +1113,11 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
   __shared__ HLane hlds[2];
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t shabuf[STD ? 16 * WG : 1];  // std_hash's per-lane SHA-256 blocks ([word][thread])
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t ln = threadIdx.x & 63;
-  const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
   // optional phase stamps of workgroup 0 (hkv_profile_phases): constant-rate
   // clock at the phase boundaries of each wave, slot STAMP_*
-  const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
-  auto mark = [&](int slot) {
-    if (stamp) clk[4 + slot] = wall_clock64();
-  };
-  if (wv == 0) mark(STAMP_START);
-
-  for (uint32_t base = blockIdx.x * PAIR_SIGS; base < n_pad; base += gridDim.x * PAIR_SIGS) {
-    if (wv == 2) {
-      // ---- the signature: u2 half (lanes 0-31), then the u1 half and A = u1 G ----
-      const uint32_t i = base + ln;
-      const bool on = ln < PAIR_SIGS;
-      uint32_t flags;
-      bool use;
-      sc sinv, m;
-      StdIn x = {};
-      sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags);
-      __threadfence_block();
-      mark(STAMP_SIG);
-      __syncthreads();  // barrier P
-      sig_wave_gsum<STD>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
-      __threadfence_block();
-      mark(STAMP_GSUM);
-      __syncthreads();  // barrier A
-      __syncthreads();  // barrier B
-      continue;
-    }
-    if (wv == 3) {
-      // ---- the key's y0 = sqrt(w) with the key's y parity (lanes 0-31) ----
-      __syncthreads();  // barrier P (nothing to wait for: the key bytes are input)
-      if (ln < PAIR_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
-      __threadfence_block();
-      mark(STAMP_SQRT);
-      __syncthreads();  // barrier A
-      __syncthreads();  // barrier B
-      continue;
-    }
-
-    // ---- chain waves: half = wv (0: k1 * Q', 1: k2 * lambda(Q')) ----
-    const int half = wv;
-    const uint32_t c = ln >> 1;                    // signature of the pair
-    const uint32_t i = base + c;
-    ge q;
-    key_point<STD>(i, n, recs, sa, q);
-    // ---- table: j*Q', j = 1..QTAB_ENTRIES, on the isomorphic curve of scale Zg ----
-    fe Zg, Qxy;
-    fe_sel(Qxy, q.x, q.y, odd);
-    pair_table(Qxy, half, odd, qlds[half], hlds[half], ln, Zg);
-    mark(half ? STAMP_TABLE1 : STAMP_TABLE0);
-    __syncthreads();  // barrier P: the signature wave's digits, r and flags are in im
-    if (half == 0) mark(STAMP_P);
-    const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
-    const bool valid = (i < n) && (flags & FLAG_VALID);
-    const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
-
-    // ---- the chain: 33 radix-16 windows, pair form ----
-    fe P, Z;
-    bool inf;
-    pair_chain(P, Z, inf, qlds[half], im, n_pad, i, valid, negh, half, odd, ln, NWIN - 1, 0);
-
-    mark(half ? STAMP_CHAIN1 : STAMP_CHAIN0);
-    // ---- join: half 1's sum to half 0 through LDS ----
-    if (half == 1) pair_publish(xch, PAIR_SIGS, c, P, Z, inf, odd);
-    fe Y, Zx;
-    fe_xch(Y, P);   // even lane: Y of the pair
-    fe_xch(Zx, Z);  // even lane: Z of the pair
-    __syncthreads();  // barrier A: half 1's sum, A and y0 are published
-    if (half == 0) mark(STAMP_A);
-    bool accept = false;
-    if (half == 0) {  // both lanes compute; the even lane's result is the verdict
-      gej acc, b;
-      acc.x = P;
-      acc.y = Y;
-      acc.z = Zx;
-      bool binf;
-      xch_read(xch, PAIR_SIGS, c, b, binf);
-      gej_add_var(acc, inf, b, binf);  // B' = u2 Q' on E_w (iso scale Zg)
-      gej A;
-      fe y0;
-      uint32_t r[8], af;
-      bool is_sq;
-      join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
-      // B = phi^-1(B') = (X, Y, Z Zg y0) on E, R = A + B exactly, x compare
-      gej bb;
-      bb.x = acc.x;
-      bb.y = acc.y;
-      fe zt;
-      fe_mul(zt, acc.z, Zg);
-      fe_mul(bb.z, zt, y0);
-      bool rinf = (af & AUXF_AINF) != 0;
-      gej_add_var(A, rinf, bb, inf);
-      accept = valid && is_sq && !rinf && x_matches_r(A.x, A.z, r) && (!STD || (af & AUXF_STDOK));
-    }
-    const uint64_t ball = __ballot(accept && !odd);
-    if (half == 0) mark(STAMP_JOIN);
-    if (half == 0 && ln == 0) {
-      const uint32_t wi = base / 32;
-      if (wi < n_words) bits[wi] = even_bits(ball);
-    }
-    __syncthreads();  // barrier B: the next group's writers of xch / aux wait for the readers
-  }
+  if (clk != nullptr && blockIdx.x == 0 && threadIdx.x == 0) clk[4 + STAMP_START] = wall_clock64();
+  for (uint32_t base = blockIdx.x * PAIR_SIGS; base < n_pad; base += gridDim.x * PAIR_SIGS)
+    pair_group<STD>(base, im, n, n_pad, gtab, bits, n_words, aux, recs, mode, clk, sa, qlds, hlds, xch, shabuf);
 }
 
 // ---------------------------------------------------------------------------
@@ -1375,7 +1381,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   if constexpr (STD) {  // the last workgroup publishes the batch's multisig record count
     if (wv == 2 && sa.ms_desc != nullptr) {
       __threadfence();
-      if (ln == 0) ms_scan_done(sa.ms_ctr, sa.ms_host, sa.ms_seq, gridDim.x);
+      if (ln == 0) ms_scan_done(sa.ms_ctr, gridDim.x);
     }
   }
 }
@@ -2094,6 +2100,112 @@ __global__ void __launch_bounds__(WG) hkv_debug_kernel(uint32_t op, uint32_t n, 
 
 }  // namespace hkv
 
+namespace hkv {
+
+// ---------------------------------------------------------------------------
+// 2e. The multisig tail (hkv_verify_std_inputs*: bare / P2SH / P2WSH /
+//     P2SH-P2WSH CHECKMULTISIG inputs). The scan (hkv_ms_scan_kernel, or the
+//     block kernel's signature wave) leaves every multisig input's desc words,
+//     its record ranges and the batch total (candidates | key checks << 32)
+//     on the device. This one launch follows it on the stream, so the host
+//     never reads the total: with no multisig input every workgroup returns
+//     at once; otherwise, separated by grid barriers,
+//       1. (fused paths, whose index pass hashed nothing) the BIP143 per-tx
+//          hashes of the batch's txs into their index rows;
+//       2. per input, its key-check records and, per signature, its sighash
+//          and candidate records (hkv_sighash_dev.h ms_emit_lane);
+//       3. the key checks (secp256k1_ec_pubkey_parse) and the candidate
+//          verifies — the pair-form group of the small-batch kernel
+//          (pair_group), one group of 32 candidates per workgroup at a time,
+//          on slot-relative scratch sized by the grid;
+//       4. per input, haskoin's countMulSig over its candidate verdicts
+//          (ms_resolve_lane), ORed into the batch's verdict words.
+//     The grid is one workgroup per CU, so every workgroup is resident at
+//     once on an otherwise idle device; the barrier's spin is bounded anyway
+//     (a workgroup that waits ~seconds gives up: the multisig verdicts then
+//     stay 0 — reject, never a false accept — and bar[2] records the fault).
+// ---------------------------------------------------------------------------
+HKV_DEV bool grid_sync(unsigned int* bar, unsigned int& sense, uint32_t* lds_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sense ^= 1u;
+    bool ok = true;
+    __threadfence();
+    if (atomicAdd(&bar[0], 1u) == gridDim.x - 1) {
+      atomicExch(&bar[0], 0u);
+      __threadfence();
+      __hip_atomic_store(&bar[1], sense, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sense) {
+        __builtin_amdgcn_s_sleep(8);
+        if (++spins > (1u << 24)) {
+          ok = false;
+          atomicExch(&bar[2], 1u);
+          break;
+        }
+      }
+    }
+    __threadfence();
+    *lds_flag = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+__global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
+  __shared__ QLane qlds[2];
+  __shared__ HLane hlds[2];
+  __shared__ uint32_t xch[25 * PAIR_SIGS];
+  __shared__ uint32_t buf[16 * PAIR_TPB];  // sha256_stream blocks ([word][thread])
+  __shared__ uint32_t okf;
+  const unsigned long long total = __hip_atomic_load(a.total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
+  if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid
+  unsigned int sense = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t tid = blockIdx.x * PAIR_TPB + threadIdx.x, nthr = gridDim.x * PAIR_TPB;
+  // 1. the BIP143 per-tx hashes (lanes: hash-major, so a wave mostly shares its hash)
+  if (a.hash_txs != TX_HASHES_NONE && a.n_tx) {
+    const uint32_t items = 3 * a.n_tx;
+    for (uint32_t b = 0; b < items; b += nthr) {
+      const uint32_t it = b + tid;
+      bool go = it < items;
+      const uint32_t t = go ? it % a.n_tx : 0, which = go ? it / a.n_tx : 0;
+      uint32_t* row = a.txt + (size_t)t * TXT_WORDS;
+      if (go && a.hash_txs == TX_HASHES_WITNESS) go = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
+      tx_hash_word_lane(a.txs, row, which, go, buf);
+    }
+    if (!grid_sync(a.bar, sense, &okf)) return;
+  }
+  // 2. key-check and candidate records
+  for (uint32_t b = 0; b < a.n; b += nthr) {
+    const uint32_t jx = b + tid;
+    ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
+                 a.cand, a.keyrec, buf);
+  }
+  if (!grid_sync(a.bar, sense, &okf)) return;
+  // 3. key checks, then the candidates in pair-form groups of 32
+  for (uint32_t b = 0; b < n_keys; b += nthr)
+    key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), b + tid, n_keys, a.kbits);
+  const uint32_t groups = (n_cand + PAIR_SIGS - 1) / PAIR_SIGS, slots = gridDim.x * PAIR_SIGS;
+  const uint32_t sbase = blockIdx.x * PAIR_SIGS;
+  const StdArgs none{};
+  for (uint32_t g = blockIdx.x; g < groups; g += gridDim.x) {
+    const uint32_t base = g * PAIR_SIGS, shift = base - sbase;  // record = slot + shift
+    pair_group<false>(sbase, a.im, n_cand - shift, slots, a.gtab, a.cbits + shift / 32, 0xFFFFFFFFu, a.aux,
+                      reinterpret_cast<uint32_t*>(a.cand) + (size_t)shift * REC_WORDS, HKV_MODE_HASKOIN, nullptr,
+                      none, qlds, hlds, xch, buf);
+  }
+  if (!grid_sync(a.bar, sense, &okf)) return;
+  // 4. the countMulSig walk
+  for (uint32_t b = 0; b < a.n; b += nthr) {
+    const uint32_t jx = b + tid;
+    ms_resolve_lane(a.desc, a.off, jx, jx < a.n, a.cbits, a.kbits, a.out_bits);
+  }
+}
+
+}  // namespace hkv
+
 // ---------------------------------------------------------------------------
 // launch wrappers (called by hkv_api.cpp)
 // ---------------------------------------------------------------------------
@@ -2134,7 +2246,7 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                        bits, n_words, aux, rw, mode, clk, StdArgs{});
   else if (split)
     hipLaunchKernelGGL(hkv_pair_split_kernel<false>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, aux, rw, mode, clk, StdArgs{});  // (record batches: no std operands)
+                       gtab, bits, n_words, aux, rw, mode, clk, StdArgs{});  // (record batches: no std operands)
   else if (mid)
     hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
   else
@@ -2149,13 +2261,11 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
                                    uint32_t n_cu, const MsScan* ms, hipStream_t st) {
-  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr, nullptr, 0ull};
+  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr};
   if (ms != nullptr && block_batch(n_pad, n_cu)) {
     sa.ms_desc = ms->desc;
     sa.ms_off = ms->off;
     sa.ms_ctr = reinterpret_cast<unsigned long long*>(ms->counters);
-    sa.ms_host = reinterpret_cast<volatile unsigned long long*>(ms->host_total);
-    sa.ms_seq = (unsigned long long)ms->seq;
   }
   uint32_t* rw = reinterpret_cast<uint32_t*>(recs);
   if (block_batch(n_pad, n_cu))
@@ -2163,12 +2273,12 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
                        bits, n_words, aux, rw, (uint32_t)HKV_MODE_HASKOIN, clk, sa);
   else
     hipLaunchKernelGGL(hkv_pair_split_kernel<true>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
-                       gtab, qs, bits, n_words, aux, rw, (uint32_t)HKV_MODE_HASKOIN, clk, sa);
+                       gtab, bits, n_words, aux, rw, (uint32_t)HKV_MODE_HASKOIN, clk, sa);
   return hipGetLastError();
 }
-hipError_t launch_pubkey_check(const void* recs, uint32_t n, uint32_t* bits, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(hkv_pubkey_check_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, (const uint32_t*)recs, n, bits);
+uint32_t ms_tail_slots(uint32_t n_cu) { return n_cu * PAIR_SIGS; }
+hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_ms_tail_kernel, dim3(n_cu), dim3(PAIR_TPB), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {

@@ -179,158 +179,13 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
                                                          const hkv_input_job* __restrict__ jobs, uint32_t n,
                                                          int32_t forkid, uint32_t* __restrict__ desc,
                                                          uint64_t* __restrict__ off,
-                                                         unsigned long long* __restrict__ counters,
-                                                         volatile unsigned long long* __restrict__ host_total,
-                                                         unsigned long long seq) {
+                                                         unsigned long long* __restrict__ counters) {
   __shared__ uint32_t buf[16 * WG];
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   ms_scan_lane(txs, n_tx, txt, scripts, scripts_len, jobs, jx, jx < n, forkid, desc, off, counters, buf);
   __threadfence();
   __syncthreads();
-  if (threadIdx.x == 0) ms_scan_done(counters, host_total, seq, gridDim.x);
-}
-
-// record: msg32 (digest byte order words) | r | s (limbs, written big-endian) |
-// pklen | pubkey | zero padding
-HKV_DEV void write_record(uint32_t* r32, const uint32_t msg[8], const uint32_t r[8], const uint32_t s[8],
-                          const uint8_t* pub, uint32_t pub_len) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    r32[k] = msg[k];
-    r32[8 + k] = __builtin_bswap32(r[7 - k]);
-    r32[16 + k] = __builtin_bswap32(s[7 - k]);
-  }
-#pragma unroll
-  for (int w = 0; w < 18; ++w) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int q = 4 * w + b;  // byte 96 + q of the record
-      uint32_t byte = 0;
-      if (q == 0) byte = pub_len;
-      else if ((uint32_t)(q - 1) < pub_len && q - 1 < 65) byte = pub[q - 1];
-      v |= byte << (8 * b);
-    }
-    r32[24 + w] = v;
-  }
-}
-
-__global__ void __launch_bounds__(WG) hkv_ms_emit_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
-                                                         const uint32_t* __restrict__ txt,
-                                                         const uint8_t* __restrict__ scripts, uint32_t scripts_len,
-                                                         const hkv_input_job* __restrict__ jobs, uint32_t n,
-                                                         int32_t forkid, const uint32_t* __restrict__ desc,
-                                                         const uint64_t* __restrict__ off64,
-                                                         uint8_t* __restrict__ cand, uint8_t* __restrict__ keyrec) {
-  __shared__ uint32_t buf[16 * WG];
-  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
-  bool go = jx < n && (desc[2 * (size_t)jx] & MS_OK);
-  MsIn r;
-  r.code = r.rd = r.wprog = scripts; r.code_len = r.rd_len = 0; r.s_eff = 0; r.mask = 0; r.n = 0;
-  r.it_off = r.it_end = 0; r.p2sh = r.wit = false;
-  const uint32_t* row = txt;
-  const uint8_t* spk = scripts;
-  uint32_t input = 0;
-  uint64_t value = 0;
-  uint32_t cbase = 0, kbase = 0;
-  if (go) {
-    const hkv_input_job jb = jobs[jx];
-    input = jb.input;
-    value = jb.value;
-    go = ms_job(jb, n_tx, txt, scripts, scripts_len, row, spk) &&
-         ms_parse(r, txs, row, jb.input, spk, jb.script_len, forkid);
-    const uint64_t o = off64[jx];
-    cbase = (uint32_t)o;
-    kbase = (uint32_t)(o >> 32);
-  }
-  // key-check records (msg, r, s zero): one per key of the script
-  if (go) {
-    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t k = 0; k < r.n; ++k) {
-      uint32_t kl;
-      const uint8_t* kp = ms_key(r.code, k, kl);
-      write_record(reinterpret_cast<uint32_t*>(keyrec + (size_t)(kbase + k) * REC_SIZE), z, z, z, kp, kl);
-    }
-  }
-  // per signature j < s_eff: its sighash, then records (msg_j, r_j, s_j, key_k), k = j..n-1
-  uint32_t off = r.it_off, idx = cbase;
-  Gen g;
-  uint32_t h[8], d[8];
-  for (uint32_t j = 0; __any(go && j < r.s_eff); ++j) {
-    const bool here = go && j < r.s_eff;
-    uint32_t d_off = 0, d_len = 0;
-    if (here) (void)ms_item(txs, r, off, d_off, d_len);
-    const bool live = here && ((r.mask >> j) & 1u);
-    uint32_t rr[8], ss[8], sh = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) rr[k] = ss[k] = 0;
-    if (live) (void)decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh);
-    JobCtx c;
-    c.forkid_form = false; c.one = false; c.single_hash = false;
-    if (live) job_setup(c, txs, row, input, sh, r.wit, forkid);  // P2WSH: BIP143 over the witness script
-    uint32_t* r32 = reinterpret_cast<uint32_t*>(cand + (size_t)idx * REC_SIZE);  // first record of sig j
-    const bool need_single = live && c.single_hash;
-    if (__any(need_single)) {
-      gen_clear(g);
-      g.T = txs; g.ooff = c.single_off; g.ocnt = 1; g.ret = PH_DONE; g.phase = PH_O_VAL;
-      sha256_stream(h, g, need_single, buf);
-      sha256d_finish(d, h);
-      if (need_single) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r32[k] = d[k];  // scratch: hashOutputs of output i
-      }
-    }
-    const bool hashed = live && !c.one;
-    if (hashed) gen_job(g, c, txs, row, r.code, r.code_len, false, value, r32);
-    else gen_clear(g);
-    sha256_stream(h, g, hashed, buf);
-    sha256d_finish(d, h);
-    if (live) {
-      uint32_t msg[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) msg[k] = hashed ? d[k] : (k == 0 ? 1u : 0u);
-      for (uint32_t k = j; k < r.n; ++k) {
-        uint32_t kl;
-        const uint8_t* kp = ms_key(r.code, k, kl);
-        write_record(reinterpret_cast<uint32_t*>(cand + (size_t)(idx++) * REC_SIZE), msg, rr, ss, kp, kl);
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ bool bit_at(const uint32_t* b, uint32_t i) { return (b[i >> 5] >> (i & 31u)) & 1u; }
-
-__global__ void __launch_bounds__(WG) hkv_ms_resolve_kernel(const uint32_t* __restrict__ desc,
-                                                            const uint64_t* __restrict__ off64, uint32_t n,
-                                                            const uint32_t* __restrict__ cbits,
-                                                            const uint32_t* __restrict__ kbits,
-                                                            uint32_t* __restrict__ out_bits) {
-  const uint32_t jx = blockIdx.x * WG + threadIdx.x;
-  if (jx >= n) return;
-  const uint32_t d0 = desc[2 * (size_t)jx];
-  if (!(d0 & MS_OK)) return;
-  const uint32_t mask = desc[2 * (size_t)jx + 1];
-  const uint32_t m = d0 & 0xFFu, nk = (d0 >> 8) & 0xFFu, s_eff = (d0 >> 16) & 0xFFu;
-  const uint64_t o = off64[jx];
-  uint32_t start = (uint32_t)o;
-  const uint32_t kbase = (uint32_t)(o >> 32);
-  bool keys_ok = true;
-  for (uint32_t k = 0; k < nk; ++k) keys_ok = keys_ok && bit_at(kbits, kbase + k);
-  // countMulSig': start = index of candidate (j, j)
-  uint32_t count = 0, j = 0;
-  for (uint32_t k = 0; k < nk; ++k) {
-    if (j >= s_eff) break;
-    if (!((mask >> j) & 1u)) {  // TxSignatureEmpty: consumes the key and the signature
-      ++j;
-      continue;
-    }
-    if (bit_at(cbits, start + (k - j))) {
-      ++count;
-      start += nk - j;
-      ++j;
-    }
-  }
-  if (keys_ok && count == m) atomicOr(&out_bits[jx >> 5], 1u << (jx & 31u));
+  if (threadIdx.x == 0) ms_scan_done(counters, gridDim.x);
 }
 
 }  // namespace hkv
@@ -376,29 +231,14 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
 // ---------------------------------------------------------------------------
 namespace hkv {
 
-// per-input desc words and record offsets; *total (zeroed here) ends as the
-// number of candidate records | key-check records << 32
+// per-input desc words and record offsets; counters[2] ends as the number of
+// candidate records | key-check records << 32 (ms_scan_done)
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
-                          uint32_t* desc, uint64_t* off, uint64_t* counters, uint64_t* host_total, uint64_t seq,
-                          hipStream_t st) {
-  if (n == 0) return hipSuccess;  // the caller publishes the empty sum itself
+                          uint32_t* desc, uint64_t* off, uint64_t* counters, hipStream_t st) {
+  if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(hkv_ms_scan_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts, scripts_len,
-                     jobs, n, forkid, desc, off, reinterpret_cast<unsigned long long*>(counters),
-                     reinterpret_cast<volatile unsigned long long*>(host_total), (unsigned long long)seq);
-  return hipGetLastError();
-}
-hipError_t launch_ms_emit(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                          uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
-                          const uint32_t* desc, const uint64_t* off, uint8_t* cand, uint8_t* keyrec, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_ms_emit_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, txs, n_tx, txt, scripts, scripts_len,
-                     jobs, n, forkid, desc, off, cand, keyrec);
-  return hipGetLastError();
-}
-hipError_t launch_ms_resolve(const uint32_t* desc, const uint64_t* off, uint32_t n, const uint32_t* cbits,
-                             const uint32_t* kbits, uint32_t* out_bits, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_ms_resolve_kernel, dim3(blocks_for(n)), dim3(WG), 0, st, desc, off, n, cbits, kbits,
-                     out_bits);
+                     jobs, n, forkid, desc, off, reinterpret_cast<unsigned long long*>(counters));
   return hipGetLastError();
 }
 

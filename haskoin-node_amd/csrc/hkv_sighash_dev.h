@@ -1353,21 +1353,191 @@ HKV_DEV void ms_scan_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const 
   }
 }
 // One thread per finished group of scanned inputs, after a device fence:
-// the last of n_groups publishes the sum to the caller's pinned host word
-// and re-arms both device counters (counters[0] the sum, counters[1] the
-// finished-group count), so the stream carries no memset and no D2H copy.
-HKV_DEV void ms_scan_done(unsigned long long* counters, volatile unsigned long long* host_total,
-                          unsigned long long seq, uint32_t n_groups) {
+// the last of n_groups moves the sum to counters[2] (where the multisig tail
+// kernel reads it: candidates | key checks << 32) and re-arms the running
+// counters (counters[0] the sum, counters[1] the finished-group count), so
+// the stream carries no memset, no D2H copy and the host waits for nothing.
+HKV_DEV void ms_scan_done(unsigned long long* counters, uint32_t n_groups) {
   unsigned long long* total = counters;
   unsigned int* done = reinterpret_cast<unsigned int*>(counters + 1);
   if (atomicAdd(done, 1u) == n_groups - 1) {
     __threadfence();
     const unsigned long long t = atomicExch(total, 0ull);
     atomicExch(done, 0u);
-    host_total[0] = t;
-    __threadfence_system();
-    host_total[1] = seq;  // the host polls this word
-    __threadfence_system();
+    atomicExch(counters + 2, t);
+    __threadfence();
+  }
+}
+
+// record: msg32 (digest byte order words) | r | s (limbs, written big-endian) |
+// pklen | pubkey | zero padding
+HKV_DEV void ms_write_record(uint32_t* r32, const uint32_t msg[8], const uint32_t r[8], const uint32_t s[8],
+                             const uint8_t* pub, uint32_t pub_len) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r32[k] = msg[k];
+    r32[8 + k] = __builtin_bswap32(r[7 - k]);
+    r32[16 + k] = __builtin_bswap32(s[7 - k]);
+  }
+#pragma unroll
+  for (int w = 0; w < 18; ++w) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int q = 4 * w + b;  // byte 96 + q of the record
+      uint32_t byte = 0;
+      if (q == 0) byte = pub_len;
+      else if ((uint32_t)(q - 1) < pub_len && q - 1 < 65) byte = pub[q - 1];
+      v |= byte << (8 * b);
+    }
+    r32[24 + w] = v;
+  }
+}
+
+// The records of one scanned multisig input (the tail kernel's emit phase):
+// one key-check record per key of its script (msg, r, s zero), then per
+// signature j < s_eff its sighash and the candidate records (msg_j, r_j, s_j,
+// key_k), k = j..n-1, at the ranges the scan allocated. Block-synchronous
+// hashing: call from wave-uniform control flow with buf = 16 * blockDim words.
+HKV_DEV void ms_emit_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const uint32_t* __restrict__ txt,
+                          const uint8_t* __restrict__ scripts, uint32_t scripts_len,
+                          const hkv_input_job* __restrict__ jobs, uint32_t jx, bool in_range, int32_t forkid,
+                          const uint32_t* __restrict__ desc, const uint64_t* __restrict__ off64,
+                          uint8_t* __restrict__ cand, uint8_t* __restrict__ keyrec, uint32_t* buf) {
+  bool go = in_range && (desc[2 * (size_t)jx] & MS_OK);
+  MsIn r;
+  r.code = r.rd = r.wprog = scripts; r.code_len = r.rd_len = 0; r.s_eff = 0; r.mask = 0; r.n = 0;
+  r.it_off = r.it_end = 0; r.p2sh = r.wit = false;
+  const uint32_t* row = txt;
+  const uint8_t* spk = scripts;
+  uint32_t input = 0;
+  uint64_t value = 0;
+  uint32_t cbase = 0, kbase = 0;
+  if (go) {
+    const hkv_input_job jb = jobs[jx];
+    input = jb.input;
+    value = jb.value;
+    go = ms_job(jb, n_tx, txt, scripts, scripts_len, row, spk) &&
+         ms_parse(r, txs, row, jb.input, spk, jb.script_len, forkid);
+    const uint64_t o = off64[jx];
+    cbase = (uint32_t)o;
+    kbase = (uint32_t)(o >> 32);
+  }
+  if (go) {
+    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t k = 0; k < r.n; ++k) {
+      uint32_t kl;
+      const uint8_t* kp = ms_key(r.code, k, kl);
+      ms_write_record(reinterpret_cast<uint32_t*>(keyrec + (size_t)(kbase + k) * REC_SIZE), z, z, z, kp, kl);
+    }
+  }
+  uint32_t off = r.it_off, idx = cbase;
+  Gen g;
+  uint32_t h[8], d[8];
+  for (uint32_t j = 0; __any(go && j < r.s_eff); ++j) {
+    const bool here = go && j < r.s_eff;
+    uint32_t d_off = 0, d_len = 0;
+    if (here) (void)ms_item(txs, r, off, d_off, d_len);
+    const bool live = here && ((r.mask >> j) & 1u);
+    uint32_t rr[8], ss[8], sh = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rr[k] = ss[k] = 0;
+    if (live) (void)decode_tx_sig(txs, d_off, d_len, forkid, rr, ss, sh);
+    JobCtx c;
+    c.forkid_form = false; c.one = false; c.single_hash = false;
+    if (live) job_setup(c, txs, row, input, sh, r.wit, forkid);  // P2WSH: BIP143 over the witness script
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(cand + (size_t)idx * REC_SIZE);  // first record of sig j
+    const bool need_single = live && c.single_hash;
+    if (__any(need_single)) {
+      gen_clear(g);
+      g.T = txs; g.ooff = c.single_off; g.ocnt = 1; g.ret = PH_DONE; g.phase = PH_O_VAL;
+      sha256_stream(h, g, need_single, buf);
+      sha256d_finish(d, h);
+      if (need_single) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r32[k] = d[k];  // scratch: hashOutputs of output i
+      }
+    }
+    const bool hashed = live && !c.one;
+    if (hashed) gen_job(g, c, txs, row, r.code, r.code_len, false, value, r32);
+    else gen_clear(g);
+    sha256_stream(h, g, hashed, buf);
+    sha256d_finish(d, h);
+    if (live) {
+      uint32_t msg[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) msg[k] = hashed ? d[k] : (k == 0 ? 1u : 0u);
+      for (uint32_t k = j; k < r.n; ++k) {
+        uint32_t kl;
+        const uint8_t* kp = ms_key(r.code, k, kl);
+        ms_write_record(reinterpret_cast<uint32_t*>(cand + (size_t)(idx++) * REC_SIZE), msg, rr, ss, kp, kl);
+      }
+    }
+  }
+}
+
+HKV_DEV bool ms_bit_at(const uint32_t* b, uint32_t i) { return (b[i >> 5] >> (i & 31u)) & 1u; }
+
+// haskoin-core countMulSig over the candidate verdicts of one input (the tail
+// kernel's last phase): all keys decode and the walk's count equals m -> the
+// input's verdict bit is set.
+HKV_DEV void ms_resolve_lane(const uint32_t* __restrict__ desc, const uint64_t* __restrict__ off64, uint32_t jx,
+                             bool in_range, const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ kbits,
+                             uint32_t* __restrict__ out_bits) {
+  if (!in_range) return;
+  const uint32_t d0 = desc[2 * (size_t)jx];
+  if (!(d0 & MS_OK)) return;
+  const uint32_t mask = desc[2 * (size_t)jx + 1];
+  const uint32_t m = d0 & 0xFFu, nk = (d0 >> 8) & 0xFFu, s_eff = (d0 >> 16) & 0xFFu;
+  const uint64_t o = off64[jx];
+  uint32_t start = (uint32_t)o;
+  const uint32_t kbase = (uint32_t)(o >> 32);
+  bool keys_ok = true;
+  for (uint32_t k = 0; k < nk; ++k) keys_ok = keys_ok && ms_bit_at(kbits, kbase + k);
+  // countMulSig': start = index of candidate (j, j)
+  uint32_t count = 0, j = 0;
+  for (uint32_t k = 0; k < nk; ++k) {
+    if (j >= s_eff) break;
+    if (!((mask >> j) & 1u)) {  // TxSignatureEmpty: consumes the key and the signature
+      ++j;
+      continue;
+    }
+    if (ms_bit_at(cbits, start + (k - j))) {
+      ++count;
+      start += nk - j;
+      ++j;
+    }
+  }
+  if (keys_ok && count == m) atomicOr(&out_bits[jx >> 5], 1u << (jx & 31u));
+}
+
+// One BIP143 per-tx hash (which: 0 hashPrevouts, 1 hashSequence, 2
+// hashOutputs) of a tx whose index row is already built, into its row (the
+// tail kernel's first phase on the fused block path, whose index pass hashed
+// nothing). Block-synchronous like ms_emit_lane.
+HKV_DEV void tx_hash_word_lane(const uint8_t* __restrict__ txs, uint32_t* __restrict__ row_out, uint32_t which,
+                               bool go, uint32_t* buf) {
+  uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (go) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[k] = row_out[k];
+    go = (row[TXT_FLAGS] & TXF_OK) != 0;
+  }
+  Gen g;
+  uint32_t h[8], d[8];
+  gen_clear(g);
+  g.T = txs;
+  if (which == 2) {
+    g.ooff = row[TXT_OUTS_FIRST]; g.ocnt = row[TXT_NOUT]; g.ret = PH_DONE; g.phase = PH_O_VAL;
+  } else {
+    g.nin = row[TXT_NIN]; g.ioff = row[TXT_INS]; g.j = 0; g.phase = which == 0 ? PH_P_IN : PH_S_IN;
+  }
+  sha256_stream(h, g, go, buf);
+  sha256d_finish(d, h);
+  if (go) {
+    const int slot = which == 0 ? TXT_HP : (which == 1 ? TXT_HS : TXT_HO);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row_out[slot + k] = d[k];
   }
 }
 

@@ -240,24 +240,21 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * d_records: scratch of n * 168 bytes; verdict bit i in d_bits
  * (>= ceil(n/64)*2 words). Multisig inputs follow haskoin-core countMulSig:
  * every (signature j, key k >= j) pair the walk could compare is verified as
- * its own record, every key of the script is parse-checked, and a resolve
- * kernel replays the walk (count == m and all keys valid). Enqueued on
- * hip_stream; the verdicts are not waited for.
- * BLOCKING: the call returns only after the multisig scan kernel it enqueues
- * has EXECUTED on hip_stream (the host needs the batch's multisig record
- * count to size the multisig work; the main verify is already enqueued
- * behind the scan while it waits). So hip_stream must be able to make
- * progress without anything this thread does after the call: a stream
- * waiting on an event recorded later by the same thread never returns.
- * While it waits the call holds only this device's sighash / std-input lock
- * (other threads' calls of the other entry points proceed; their work is
- * ordered between this call's main verify and its multisig work).
- * n <= 2^32 / 136 (31,580,641) inputs: a 16-of-16 input yields 136 candidate
- * records and the batch's candidate sum is a 32-bit device counter. */
+ * its own record, every key of the script is parse-checked, and the walk is
+ * replayed on device (count == m and all keys valid).
+ * ASYNCHRONOUS: everything is enqueued on hip_stream and the call returns
+ * without waiting for any of it (the batch's multisig record count stays on
+ * the device: one tail launch reads it and does nothing when it is 0), so a
+ * caller may enqueue block k+1 while block k verifies, and hip_stream may be
+ * gated on events recorded after the call. Batches run in chunks of 131,072
+ * inputs (the multisig scratch is sized per chunk by its 16-of-16 bound, 136
+ * candidate + 16 key-check records per input, allocated on first use).
+ * n <= 0xFFFFFF00. */
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                                  int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream);
 /* Host-memory form of the above; writes ceil(n/32) verdict words. Blocking.
- * Same bound on n. */
+ * Same bound on n. HKV_E_INTERNAL if the multisig tail's grid barrier gave up
+ * (its workgroups were not co-resident: the multisig verdicts stayed 0). */
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
                           uint32_t* verdict_bits);
 

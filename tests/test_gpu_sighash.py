@@ -468,3 +468,100 @@ def test_wrapped_single_sig_vs_oracle(torch, ver, coracle, forkid):
     assert got == want, [(names[k], got[k], want[k]) for k in range(len(jobs)) if got[k] != want[k]][:10]
     assert _device_verify_std(torch, ver, raw, jobs, forkid) == got
     assert sum(got) >= 6 * 4 and len(got) - sum(got) >= 6 * 5
+
+
+def _ms_mix(rng, forkid):
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(24)]
+    mtxs, mjobs, names = txgen.multisig_cases(rng, keys, forkid)
+    return [sh.tx_serialize(t) for t in mtxs], mjobs, names
+
+
+@pytest.mark.parametrize("n_tx,forkid", [(3000, None), (3000, 0), (20000, None)])
+def test_multisig_on_every_launch_shape(torch, ver, coracle, n_tx, forkid):
+    """The multisig cases (bare, P2SH, P2WSH, P2SH-P2WSH; valid and
+    adversarial) inside batches past the block kernel's bound: ~5,500 inputs
+    take the fused pair kernel with the separate scan kernel (that
+    path had no multisig GPU test), ~37,000 the extraction kernel and the
+    full-grid verify. Host and device entry points: the multisig verdicts
+    equal the oracle's countMulSig walk, every generated single-signature
+    input verifies."""
+    import hkv
+    from hkv import blockgen
+    rng = random.Random(1313 + n_tx + (forkid or 0))
+    btxs, bjobs = blockgen.make_block(ver, torch, n_tx=n_tx, seed=blockgen.SEED + 7 * n_tx)
+    mraw, mjobs, names = _ms_mix(rng, forkid)
+    raw = btxs + mraw
+    jobs = list(bjobs) + [(t + len(btxs), i, p, v) for (t, i, p, v) in mjobs]
+    order = list(range(len(jobs)))
+    rng.shuffle(order)
+    jobs = [jobs[k] for k in order]
+    is_ms = [k >= len(bjobs) for k in order]
+    assert len(jobs) > 16 * 256
+    want_ms = _ms_oracle(coracle, mraw, mjobs, forkid)
+    want = [None] * len(jobs)
+    for pos, k in enumerate(order):
+        want[pos] = want_ms[k - len(bjobs)] if k >= len(bjobs) else True
+    got = hkv.verify_std_inputs(ver, raw, jobs, forkid)
+    if forkid is None:
+        bad = [(names[order[p] - len(bjobs)] if is_ms[p] else "single", got[p], want[p])
+               for p in range(len(jobs)) if got[p] != want[p]]
+        assert not bad, bad[:10]
+    else:  # the device generator's singles sign without the fork id: only the multisig verdicts are meaningful
+        bad = [(names[order[p] - len(bjobs)], got[p], want[p]) for p in range(len(jobs)) if is_ms[p] and got[p] != want[p]]
+        assert not bad, bad[:10]
+    assert _device_verify_std(torch, ver, raw, jobs, forkid) == got
+    assert sum(g for g, m in zip(got, is_ms) if m) > 80
+
+
+def test_std_inputs_device_returns_before_the_stream_runs(torch, ver, coracle):
+    """hkv_verify_std_inputs_device only enqueues: with
+    the call's stream gated behind ~20 full-grid verifies on another stream
+    (an event wait), the call returns long before the gate opens, and once it
+    has run the verdicts — multisig inputs included, whose count the host
+    never reads — equal the oracle's."""
+    import time
+    import hkv
+    from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
+    rng = random.Random(2024)
+    mraw, mjobs, _ = _ms_mix(rng, None)
+    keys = [txgen.Key(rng.randrange(1, o.N)) for _ in range(8)]
+    btxs, bjobs = txgen.std_block(rng, 40, keys, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
+    raw = [sh.tx_serialize(t) for t in btxs] + mraw
+    jobs = list(bjobs) + [(t + len(btxs), i, p, v) for (t, i, p, v) in mjobs]
+    want = _ms_oracle(coracle, raw, jobs, None)
+    tb = TxBatch(raw)
+    arr = np.zeros(len(jobs), dtype=INPUT_JOB_DTYPE)
+    for k, (t, i, spk, value) in enumerate(jobs):
+        off, ln = tb.script(spk)
+        arr[k] = (t, i, off, ln, value)
+    _, pool = tb.struct()
+    d_bytes, d_off, d_pool, d_jobs = upload(torch, tb.bytes), upload(torch, tb.offsets), upload(torch, pool), \
+        upload(torch, arr)
+    dt = hkv.HkvTxs(d_bytes.data_ptr(), d_off.data_ptr(), len(raw), d_pool.data_ptr(), tb._len)
+    recs = torch.zeros(len(jobs) * 168, dtype=torch.uint8, device="cuda")
+    bits = torch.zeros(((len(jobs) + 63) // 64) * 2, dtype=torch.int32, device="cuda")
+    # the gate: full-grid verifies of 1M records on another stream, ~9 ms each
+    n_big = 1 << 20
+    big = torch.empty(n_big * 168, dtype=torch.uint8, device="cuda")
+    bbits = torch.zeros(n_big // 32 + 2, dtype=torch.int32, device="cuda")
+    ver.gen_records_device(0, 77, n_big, 4096, 100, big.data_ptr())
+    gate, s = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        ver.verify_device(0, big.data_ptr(), n_big, 0, bbits.data_ptr(), gate.cuda_stream)
+    ev = torch.cuda.Event()
+    ev.record(gate)
+    s.wait_event(ev)
+    t1 = time.perf_counter()
+    ver.verify_std_inputs_device(0, dt, d_jobs.data_ptr(), len(jobs), -1, recs.data_ptr(), bits.data_ptr(),
+                                 s.cuda_stream)
+    t_call = time.perf_counter() - t1
+    torch.cuda.synchronize()
+    t_gate = time.perf_counter() - t0
+    assert t_gate > 0.1, t_gate
+    assert t_call < 0.25 * t_gate, (t_call, t_gate)
+    w = bits.cpu().numpy().view(np.uint32)
+    got = [bool((w[k // 32] >> (k % 32)) & 1) for k in range(len(jobs))]
+    assert got == want
+    assert int(bbits[: n_big // 32].cpu().numpy().view(np.uint32).astype(np.uint64).sum()) == (n_big // 32) * 0xFFFFFFFF

@@ -2,12 +2,16 @@
 // multiply (tools/ubench_int.hip measured the products; its carry rows ran one
 // serial VCC chain, so they priced latency, not issue). Every lane runs CH
 // independent chains, each with its own carry SGPR pair, so the numbers are
-// SIMD issue cycles per wave64 instruction at 8 waves/SIMD.
+// SIMD issue cycles per wave64 instruction at 8 waves/SIMD; round 4 adds the
+// same table at ONE wave per SIMD (the block kernel's regime: a lone wave pays
+// an op's issue cost and its dependent latency, nothing hides either) and
+// dependent-chain rows for the carry, DPP and 24-bit multiply forms.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 tools/ubench_ops.hip -o tools/ubench_ops
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <algorithm>
 #include <vector>
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -19,7 +23,8 @@ constexpr int CH = 8;
 struct Stamp { unsigned long long t0, t1, r0, r1; };
 
 // instructions per chain step for each op
-static const int NINSTR[] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 3, 1, 1};
+static const int NINSTR[] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 3, 1, 1,
+                             1, 1, 1, 1, 2, 1, 1, 1};
 static const char* NAMES[] = {
     "v_add_u32",                        // 0
     "v_add_co_u32_e64 (sdst)",          // 1
@@ -55,6 +60,14 @@ static const char* NAMES[] = {
     "mad(co->vcc)+addc_e32, 1 instr apart, no nop",  // 31
     "v_cndmask_b32_e32 (vcc from v_cmp_e32 each 8)",  // 32
     "v_cndmask_b32_e64 (s pair from v_cmp_e64 each 8)",  // 33
+    "v_mov_b32_dpp quad_perm (independent)",  // 34
+    "v_mad_u32_u24",                    // 35
+    "v_mul_hi_u32",                     // 36
+    "v_add3_u32 dependent chain (1/lane)",  // 37
+    "v_addc_co_u32_e64 dependent SGPR-carry chain + s_nop 1 (1/lane)",  // 38
+    "v_mov_b32_dpp dependent chain (1/lane)",  // 39
+    "v_mad_u32_u24 dependent chain (1/lane)",  // 40
+    "v_lshl_add_u64 dependent chain (1/lane)",  // 41
 };
 
 template <int OP>
@@ -190,6 +203,23 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
       } else if constexpr (OP == 33) {
         if (k == 0) asm volatile("v_cmp_gt_u32_e64 s[20:21], %0, %1" : : "v"(a[7]), "v"(b) : "s20", "s21");
         asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a[k]) : "v"(h[k]));
+      } else if constexpr (OP == 34) {
+        asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(a[k]) : "v"(h[(k + 1) % CH]));
+        asm volatile("" : "+v"(h[(k + 1) % CH]));
+      } else if constexpr (OP == 35) {
+        asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b), "v"(h[k]));
+      } else if constexpr (OP == 36) {
+        asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[k]) : "v"(b));
+      } else if constexpr (OP == 37) {
+        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[0]) : "v"(b), "v"(h[k]));
+      } else if constexpr (OP == 38) {
+        asm volatile("v_addc_co_u32_e64 %0, s[20:21], %0, %1, s[20:21]\n\ts_nop 1" : "+v"(a[0]) : "v"(b) : "s20", "s21");
+      } else if constexpr (OP == 39) {
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a[0]));
+      } else if constexpr (OP == 40) {
+        asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a[0]) : "v"(b), "v"(h[k]));
+      } else if constexpr (OP == 41) {
+        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[0]) : "v"(acc[(k + 1) % CH]));
       }
     }
   }
@@ -203,8 +233,8 @@ __global__ void __launch_bounds__(256) kern(uint32_t seed, uint32_t* out, Stamp*
 }
 
 template <int OP>
-int run(int n_cu) {
-  const int threads = 256, blocks = n_cu * 8;  // 8 waves per SIMD
+int run(int n_cu, int wps) {
+  const int threads = 256, blocks = n_cu * wps;  // wps waves per SIMD (a block: one wave on each of 4 SIMDs)
   uint32_t* out; Stamp* st;
   CHECK(hipMalloc(&out, sizeof(uint32_t) * threads * blocks));
   CHECK(hipMalloc(&st, sizeof(Stamp) * blocks));
@@ -219,14 +249,22 @@ int run(int n_cu) {
   std::vector<Stamp> hs(blocks);
   CHECK(hipMemcpy(hs.data(), st, sizeof(Stamp) * blocks, hipMemcpyDeviceToHost));
   double clk = 0; int nc = 0;
-  for (auto& s : hs) if (s.r1 > s.r0) { clk += (double)(s.t1 - s.t0) / (double)(s.r1 - s.r0) * 100e6; ++nc; }
+  std::vector<double> loop;  // in-kernel shader cycles of one block's loop (s_memtime)
+  for (auto& s : hs) if (s.r1 > s.r0) {
+    clk += (double)(s.t1 - s.t0) / (double)(s.r1 - s.r0) * 100e6; ++nc;
+    loop.push_back((double)(s.t1 - s.t0));
+  }
   clk /= nc;
+  std::sort(loop.begin(), loop.end());
   // SIMD cycles per wave-instruction: cycles * SIMDs / (waves * instructions)
   const double waves = (double)reps * blocks * (threads / 64);
   const double instr_per_wave = (double)ITERS * CH * NINSTR[OP];
   const double cyc = ms * 1e-3 * clk * (n_cu * 4.0) / (waves * instr_per_wave);
-  printf("{\"op\": \"%s\", \"simd_cycles_per_wave_instr\": %.2f, \"instr_per_step\": %d, \"clk_ghz\": %.3f}\n",
-         NAMES[OP], cyc, NINSTR[OP], clk * 1e-9);
+  // the same from the loop's own clock (no launch overhead): wps waves share a SIMD
+  const double cyc_loop = loop.empty() ? 0.0 : loop[loop.size() / 2] / (instr_per_wave * wps);
+  printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"simd_cycles_per_wave_instr\": %.2f, "
+         "\"loop_cycles_per_wave_instr\": %.2f, \"instr_per_step\": %d, \"clk_ghz\": %.3f}\n",
+         NAMES[OP], wps, cyc, cyc_loop, NINSTR[OP], clk * 1e-9);
   CHECK(hipFree(out)); CHECK(hipFree(st));
   return 0;
 }
@@ -234,16 +272,22 @@ int run(int n_cu) {
 int main() {
   hipDeviceProp_t p; if (hipGetDeviceProperties(&p, 0) != hipSuccess) { fprintf(stderr, "no device\n"); return 1; }
   const int n_cu = p.multiProcessorCount;
-  printf("# device %s CUs %d; SIMD cycles per wave64 instruction, 8 independent chains/lane, 8 waves/SIMD\n",
-         p.gcnArchName, n_cu);
+  printf("# device %s CUs %d; SIMD cycles per wave64 instruction, 8 independent chains/lane (or one, the "
+         "dependent rows), at 8 and at 1 wave(s) per SIMD\n", p.gcnArchName, n_cu);
   int rc = 0;
-  rc |= run<0>(n_cu); rc |= run<1>(n_cu); rc |= run<2>(n_cu); rc |= run<3>(n_cu); rc |= run<4>(n_cu);
-  rc |= run<5>(n_cu); rc |= run<6>(n_cu); rc |= run<7>(n_cu); rc |= run<8>(n_cu); rc |= run<9>(n_cu);
-  rc |= run<10>(n_cu); rc |= run<11>(n_cu); rc |= run<12>(n_cu); rc |= run<13>(n_cu); rc |= run<14>(n_cu);
-  rc |= run<15>(n_cu); rc |= run<16>(n_cu); rc |= run<17>(n_cu); rc |= run<18>(n_cu); rc |= run<19>(n_cu);
-  rc |= run<20>(n_cu); rc |= run<21>(n_cu); rc |= run<22>(n_cu); rc |= run<23>(n_cu); rc |= run<24>(n_cu);
-  rc |= run<25>(n_cu); rc |= run<26>(n_cu); rc |= run<27>(n_cu); rc |= run<28>(n_cu); rc |= run<29>(n_cu);
-  rc |= run<30>(n_cu); rc |= run<31>(n_cu); rc |= run<32>(n_cu); rc |= run<33>(n_cu);
+  for (int wps : {8, 1}) {
+    rc |= run<0>(n_cu, wps); rc |= run<1>(n_cu, wps); rc |= run<2>(n_cu, wps); rc |= run<3>(n_cu, wps);
+    rc |= run<4>(n_cu, wps); rc |= run<5>(n_cu, wps); rc |= run<6>(n_cu, wps); rc |= run<7>(n_cu, wps);
+    rc |= run<8>(n_cu, wps); rc |= run<9>(n_cu, wps); rc |= run<10>(n_cu, wps); rc |= run<11>(n_cu, wps);
+    rc |= run<12>(n_cu, wps); rc |= run<13>(n_cu, wps); rc |= run<14>(n_cu, wps); rc |= run<15>(n_cu, wps);
+    rc |= run<16>(n_cu, wps); rc |= run<17>(n_cu, wps); rc |= run<18>(n_cu, wps); rc |= run<19>(n_cu, wps);
+    rc |= run<20>(n_cu, wps); rc |= run<21>(n_cu, wps); rc |= run<22>(n_cu, wps); rc |= run<23>(n_cu, wps);
+    rc |= run<24>(n_cu, wps); rc |= run<25>(n_cu, wps); rc |= run<26>(n_cu, wps); rc |= run<27>(n_cu, wps);
+    rc |= run<28>(n_cu, wps); rc |= run<29>(n_cu, wps); rc |= run<30>(n_cu, wps); rc |= run<31>(n_cu, wps);
+    rc |= run<32>(n_cu, wps); rc |= run<33>(n_cu, wps); rc |= run<34>(n_cu, wps); rc |= run<35>(n_cu, wps);
+    rc |= run<36>(n_cu, wps); rc |= run<37>(n_cu, wps); rc |= run<38>(n_cu, wps); rc |= run<39>(n_cu, wps);
+    rc |= run<40>(n_cu, wps); rc |= run<41>(n_cu, wps);
+  }
   return rc;
 }
 
