@@ -367,6 +367,64 @@ def host_path(v, recs, n: int, steps: int) -> dict:
         v.lib.hkv_batch_free(b)
 
 
+def inproc_leg(v, torch, n: int, steps: int) -> dict:
+    """The multi-device path the Haskell binding uses: ONE
+    process opens every visible GPU through hkv_open(0, ...) and verifies
+    BASELINE configs[4]'s 16,777,216-record batch from one pinned host batch
+    with hkv_verify — contiguous 64-aligned shards per device, H2D pipelined
+    with the verify on each device, verdict words merged on the host (D2H, no
+    RCCL inside libhkv). PCIe-inclusive; checked against the construction
+    labels. On one GPU it is the N = 1 point of that path."""
+    import numpy as np
+    import hkv
+    # the records and labels on device 0 of the bench's own context, then to
+    # the pinned batch of the all-device context
+    recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
+    labels = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
+    v.gen_batch_device(0, CONFIG4_SEED, 0, n, POOL, UNC_PERMILLE, CONFIG4_INVALID_PERMILLE, recs.data_ptr(),
+                       labels.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = recs.cpu().numpy()
+    lab = labels.cpu().numpy().view(np.uint32)[: (n + 31) // 32].copy()
+    del recs, labels
+    torch.cuda.empty_cache()
+    va = hkv.Verifier(hkv.VerifierConfig(device_ids=None, flags=1))
+    try:
+        nd = va.lib.hkv_ctx_num_devices(va.ctx)
+        b = ctypes.c_void_p()
+        rc = va.lib.hkv_batch_alloc(va.ctx, n, ctypes.byref(b))
+        if rc != 0:
+            return {"error": rc}
+        try:
+            ctypes.memmove(va.lib.hkv_batch_records(b), host.ctypes.data, n * 168)
+            del host
+            words = np.zeros((n + 31) // 32, dtype=np.uint32)
+            wp = words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+            rc = va.lib.hkv_verify(va.ctx, b, n, 0, wp)  # warm-up (allocations)
+            if rc != 0:
+                return {"error": rc}
+            k = max(2, steps // 5)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                va.lib.hkv_verify(va.ctx, b, n, 0, wp)
+            dt = (time.perf_counter() - t0) / k
+            last = (n % 32) and ((1 << (n % 32)) - 1)
+            diff = words ^ lab
+            if last:
+                diff[-1] &= last
+            mism = int(np.unpackbits(diff.view(np.uint8)).sum())
+            return {"devices": nd, "records": n, "ms": round(dt * 1e3, 2), "verifies_per_s": round(n / dt, 1),
+                    "mismatches_vs_labels": mism, "accepted": int(np.unpackbits(words.view(np.uint8)).sum()),
+                    "h2d_bytes": n * 168,
+                    "workload": "BASELINE configs[4] batch (16,777,216 records, 5% invalid) from one pinned host "
+                                "batch: hkv_open(all visible GPUs) + hkv_verify, PCIe-inclusive, verdict words "
+                                "merged on the host"}
+        finally:
+            va.lib.hkv_batch_free(b)
+    finally:
+        va.close()
+
+
 def header_batches(v, torch, steps: int) -> dict:
     """importHeaders' per-header work (headerHash +
     isValidPOW + linkage) for a 2,000-header peer message (a chained bchRegTest
@@ -654,6 +712,9 @@ def main() -> None:
     ap.add_argument("--no-headers", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-inproc", action="store_true",
+                    help="skip the in-process all-GPU leg (hkv_open over every visible GPU, configs[4] from a pinned "
+                         "host batch)")
     ap.add_argument("--config4", action="store_true",
                     help="BASELINE configs[4] (16,777,216 records, 5%% invalid, seed 0x484B5635, sharded over the "
                          "ranks); the default whenever WORLD_SIZE > 1")
@@ -798,6 +859,9 @@ def main() -> None:
             mkl = merkle_batches(v, torch, args.steps)
         if single and not args.no_adversarial:
             adv, adv_recs, adv_got = adversarial_mix(v, torch, n, sptr, args.steps)
+        inproc = None
+        if single and not args.no_inproc:
+            inproc = inproc_leg(v, torch, args.config4_n, args.steps)
         cpu = None
         if single and not args.no_cpu_baseline:
             samples = []
@@ -885,6 +949,7 @@ def main() -> None:
             "headers": hdr,
             "merkle": mkl,
             "host_path": hp,
+            "inproc": inproc,
         }
         print(json.dumps(line), flush=True)
     v.close()

@@ -243,12 +243,13 @@ HKV_DEV bool pair_odd(bool f) { return dpp_bc1(f ? 1u : 0u) != 0; }
 // form with the small multiples gathered into one lane-parallel step: with
 // A = X^2, B = Y^2, M = X B, C = B^2 (dbl-2009-l: E = 3A, S = 4M)
 //   X3 = 9A^2 - 8M,  Y3 = A (36M - 27A^2) - 8C,  Z3 = 2YZ.
-// Products [A | B], [M | YZ], [C | A^2], then [X3 | D] and [8C | 2YZ] side
-// by side (two interleaved small-multiple chains, one shift), [. | A D],
-// [. | Y3]: 2S + 2M deep with two subtractions, where the halved form
-// needed 3A, /2, 2M and three subtractions (tools/ubench_chain.hip).
+// Products [A | B], [M | YZ], [C | A^2], then [X3 | D] as one fused pass
+// (fe_lin2: both small multiples and the difference) beside [8C | 2YZ] (one
+// shift), and [. | A D - 8C] as one product with an addend (fe_mul_add): 2S + 2M
+// deep with no separate subtraction chain, where the halved form needed 3A,
+// /2, 2M and three subtractions (tools/ubench_chain.hip).
 HKV_DEV void pair_double(fe& P, fe& Z, uint32_t odd) {
-  fe R1, T, O1, R2, R3, P1, P2, u, w, r, Q, t, Y3;
+  fe R1, T, O1, R2, R3, P1, P2, r, Q, t;
   fe_sqr(R1, P);              // A              | B
   fe_xch(T, R1);              // B              | A
   fe_sel(O1, T, Z, odd);      // B              | Z
@@ -257,13 +258,12 @@ HKV_DEV void pair_double(fe& P, fe& Z, uint32_t odd) {
   fe_sel(P2, R2, R3, odd);    // M              | A^2
   fe_xch(P1, P2);             // A^2            | M
   fe_sel(O1, R3, R2, odd);    // C              | YZ
-  fe_mul_small2(u, P1, odd ? 36u : 9u, w, P2, odd ? 27u : 8u);
+  fe_lin2(r, P1, odd ? 36u : 9u, P2, odd ? 27u : 8u);  // X3 | D = 36M - 27A^2
   fe_shl_var(Q, O1, odd ? 1u : 3u);   // 8C | 2YZ
-  fe_sub(r, u, w);            // X3             | D = 36M - 27A^2
-  fe_mul(t, T, r);            //                | A D
-  fe_xch(O1, Q);              //                | 8C
-  fe_sub(Y3, t, O1);          //                | Y3
-  fe_sel(P, r, Y3, odd);
+  fe_xch(O1, Q);              // 2YZ            | 8C
+  fe_cneg(O1, O1, odd != 0);  //                | -8C
+  fe_mul_add(t, T, r, O1);    //                | Y3 = A D - 8C
+  fe_sel(P, r, t, odd);
   Z = Q;                      //                | Z3
 }
 
@@ -327,14 +327,16 @@ HKV_DEV void fe_quad(fe& r, const fe& a) {
 }
 constexpr int QP_0 = 0x00, QP_3 = 0xFF, QP_0112 = 0xD4;  // [0,0,0,0] [3,3,3,3] [0,1,1,3]
 constexpr int QP_1100 = 0x05, QP_3021 = 0x63, QP_0333 = 0xFC;  // [1,1,0,0] [3,0,2,1] [0,3,3,3]
+constexpr int QP_0331 = 0x7C;                                   // [0,3,3,1]
 // 2V in the unhalved form of pair_double: [A | B | . | .], then
-// [M | C | YZ | A^2] on the four lanes, [X3 | D | Z3 | 8C] by two
-// interleaved small-multiple chains and one subtraction, [. | A D | . | .],
-// [. | Y3 | . | .]: S + 2M deep. Operands that are one quad permutation of a
-// product are formed by a single DPP move per limb (P1, P2), and the others
-// by two permutations and one select, not by broadcasts and select chains.
+// [M | C | YZ | A^2] on the four lanes, [X3 | D | Z3 | -8C] by one fused
+// small-multiple difference (fe_lin2), [. | Y3 = A D - 8C | . | .] by one
+// product with an addend (fe_mul_add): S + 2M deep. Operands that are one
+// quad permutation of a product are formed by a single DPP move per limb
+// (P1, P2), and the others by two permutations and one select, not by
+// broadcasts and select chains.
 HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
-  fe R1, Aq, RA, T, opA, opB, R2, P1, P2, u, w, r, t, C8, Y3;
+  fe R1, Aq, RA, T, opA, opB, R2, P1, P2, r, t, C8;
   fe_sqr(R1, V);              // A = X^2 | B = Y^2 | . | .
   fe_quad<QP_0>(Aq, R1);      // A        | A      | A  | A
   fe_quad<QP_1100>(RA, R1);   // B        | B      | A  | A
@@ -343,15 +345,13 @@ HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
   fe_sel(opB, RA, V, m2);         // B | B | Z | A
   fe_mul(R2, opA, opB);       // M | C | YZ | A^2
   fe_quad<QP_3021>(P1, R2);   // A^2 | M | YZ | C
-  fe_quad<QP_0333>(P2, R2);   // M | A^2 | . | .
-  const uint32_t k1 = m0 ? 9u : (m1 ? 36u : (m2 ? 2u : 8u));
-  const uint32_t k2 = m0 ? 8u : (m1 ? 27u : 0u);
-  fe_mul_small2(u, P1, k1, w, P2, k2);
-  fe_sub(r, u, w);            // X3 | D = 36M - 27A^2 | Z3 = 2YZ | 8C
-  fe_mul(t, Aq, r);           // . | A D | . | .
-  fe_quad<QP_3>(C8, r);
-  fe_sub(Y3, t, C8);          // . | Y3 | . | .
-  fe_sel(V, r, Y3, m1);       // X3 | Y3 | Z3 | .
+  fe_quad<QP_0331>(P2, R2);   // M | A^2 | . | C
+  const uint32_t k1 = m0 ? 9u : (m1 ? 36u : (m2 ? 2u : 0u));
+  const uint32_t k2 = m0 ? 8u : (m1 ? 27u : (m2 ? 0u : 8u));
+  fe_lin2(r, P1, k1, P2, k2); // X3 | D = 36M - 27A^2 | Z3 = 2YZ | -8C
+  fe_quad<QP_3>(C8, r);       // -8C on every lane
+  fe_mul_add(t, Aq, r, C8);   // . | Y3 = A D - 8C | . | .
+  fe_sel(V, r, t, m1);        // X3 | Y3 | Z3 | .
 }
 
 // P += TXY in place for a table build: TXY affine on the curve of the

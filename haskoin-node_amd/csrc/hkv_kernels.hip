@@ -1356,16 +1356,27 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       blk_post(&bflag[BF_U], seq);
     } else {
       // ---- R = U + phi^-1(S_hi) on E, the x compare, the verdicts ----
-      blk_wait(&bflag[BF_U], seq);
+      // (the join inputs and S_hi's scale on E are formed before U arrives:
+      // A and y0 were published long before this chain ended)
+      blk_wait(&bflag[BF_A], seq);
+      blk_wait(&bflag[BF_Y], seq);
       bool accept = false;
+      gej A;
+      fe y0, zb;
+      uint32_t r[8], af;
+      bool is_sq;
       if (half == 0) {
-        gej A;
-        fe y0, PR, ZR;
-        uint32_t r[8], af;
-        bool is_sq, rinf;
         join_inputs(im, aux, n_pad, i, A, y0, r, af, is_sq);
+        fe zt;
+        fe_mul(zt, Zs, zs);
+        fe_mul(zb, zt, y0);
+      }
+      blk_wait(&bflag[BF_U], seq);
+      if (half == 0) {
+        fe PR, ZR;
+        bool rinf;
         pair_from_xch(xch[4], c, odd, PR, ZR, rinf);
-        add_segment(PR, ZR, rinf, P, Zs, inf, zs, y0, odd);
+        pair_add_var(PR, ZR, rinf, P, zb, inf, odd);
         // the even lane holds X
         accept = valid && is_sq && !rinf && x_matches_r(PR, ZR, r) && (!STD || (af & AUXF_STDOK));
       }

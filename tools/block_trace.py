@@ -38,6 +38,7 @@ def report(d: str) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--batch32", action="store_true", help="also the 64,000-tx batch (bench block_mix.batch32)")
     ap.add_argument("--report", default=None, help="summarise a rocprofv3 csv output directory")
     a = ap.parse_args()
     if a.report:
@@ -50,6 +51,8 @@ def main():
     st = torch.cuda.Stream()
     blocks = (("configs0", blockgen.make_p2pkh_block(v, torch)),
               ("configs2", blockgen.make_block(v, torch, n_tx=2000, seed=blockgen.SEED + 2000)))
+    if a.batch32:
+        blocks += (("batch32", blockgen.make_block(v, torch, n_tx=64000, seed=blockgen.SEED + 64000)),)
     for name, (txs, inputs) in blocks:
         db = blockgen.DeviceBlock(torch, txs, inputs)
         for what in ("verify", "extract"):

@@ -230,13 +230,19 @@ def scan_block(pairs, mode):
     lines = []
     if mode == "acc":
         pre_ins = []
-    elif mode == "red0":
+    elif mode in ("red0", "red0e"):
         pre_ins = ['"v"(h[0])', '"s"(k977)']
         lines.append("v_mad_u64_u32 %0, %2, %5, %6, 0")
+        if mode == "red0e":  # + the addend's limb 0 (the sum stays below 2^43)
+            pre_ins.append('"v"(ej)')
+            lines.append("v_mad_u64_u32 %0, %2, %7, 1, %0")
     else:
         pre_ins = ['"v"(prevhi)', '"v"(init)', '"v"(hj)', '"s"(k977)']
         lines.append("v_mad_u64_u32 %0, %2, %5, 1, %6")
         lines.append("v_mad_u64_u32 %0, %2, %7, %8, %0")
+        if mode == "rede":  # + the addend's limb j
+            pre_ins.append('"v"(ej)')
+            lines.append("v_mad_u64_u32 %0, %2, %9, 1, %0")
     base = 5 + len(pre_ins)
     ref = lambda nm: f"%{base + regs[nm]}"
     m = len(pairs)
@@ -271,15 +277,16 @@ def scan_block(pairs, mode):
             f'      : {ins});')
 
 
-def reduced_scan(name, cols, doc):
+def reduced_scan(name, cols, doc, addend=False):
     """A 256x256 product given as column pair lists cols[0..14], reduced mod p
     on the fly: columns 8..14 are scanned first (their carry-in from column 7
     is deferred), giving the high half h[0..7]; columns 0..7 then fold
     h * 2^256 == h * (2^32 + 977) into their accumulators (h[j] * 977 and
     h[j-1] enter column j). Output: r[0..7] and T < 2^38 with
     a * b == r + T * 2^256 (mod p)."""
+    sig = "uint32_t r[8], uint64_t& T, const uint32_t* a, const uint32_t* b" + (", const uint32_t* e" if addend else "")
     out = [""] + ["// " + l for l in doc] + [
-        f"__device__ __forceinline__ void {name}(uint32_t r[8], uint64_t& T, const uint32_t* a, const uint32_t* b) {{",
+        f"__device__ __forceinline__ void {name}({sig}) {{",
         "  uint64_t acc = 0;",
         "  uint32_t top;",
         "  uint64_t c0, c1, c2;",
@@ -305,13 +312,15 @@ def reduced_scan(name, cols, doc):
         out.append(f"  // column {j}: {len(cols[j])} products + h[{j}] * 977" + (f" + h[{j - 1}]" if j else ""))
         out.append("  {")
         out.append("    uint64_t accn;")
+        if addend:
+            out.append(f"    const uint32_t ej = e[{j}];")
         if j:
             out.append("    const uint32_t prevhi = (uint32_t)(acc >> 32);")
             out.append(f"    const uint64_t init = ((uint64_t)top << 32) | h[{j - 1}];")
             out.append(f"    const uint32_t hj = h[{j}];")
-            blk = scan_block(cols[j], "red")
+            blk = scan_block(cols[j], "rede" if addend else "red")
         else:
-            blk = scan_block(cols[j], "red0")
+            blk = scan_block(cols[j], "red0e" if addend else "red0")
         out.append("  " + blk.replace("\n", "\n  "))
         out.append("    acc = accn;")
         out.append("  }")
@@ -339,6 +348,10 @@ def reduced_functions():
         "a * b mod p with the reduction folded into the product scan (HKV_MUL_RED):",
         "no separate 8-mad reduction chain, its limb moves or its two 8-limb",
         "add chains; a column's carry-in and h[j-1] enter through one mad (x 1)."])
+    out += reduced_scan("mul256_red_add_ps", mul_cols, [
+        "a * b + e mod p (e < 2^256): mul256_red_ps with the addend's limb j",
+        "entering low column j through one more mad (x 1) — a product and an",
+        "addition for one extra instruction per low column, no carry chain."], addend=True)
     out += reduced_scan("sqr256_red_ps", sqr_cols[:15], [
         "a^2 mod p as a column scan of 43 products (8 squares, 7 a_i * 2a_{i+1},",
         "28 a_i * (2a)_j limbs incl. the 1-bit limb 8) instead of 36 products plus",
