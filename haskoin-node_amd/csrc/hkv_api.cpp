@@ -21,6 +21,10 @@
 #include "hkv_layout.h"
 #include "hkv_plan.h"
 
+#ifndef HKV_STD_OVERLAP
+#define HKV_STD_OVERLAP 1
+#endif
+
 namespace {
 
 thread_local std::string g_last_hip;
@@ -30,6 +34,11 @@ struct DevCtx {
   int n_cu = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // H2D of host batches, overlapped with verify
+  // the hash half of a large standard-input batch runs here beside the
+  // ECDSA kernels (enqueue_std_chunk), forked from and joined back into the
+  // caller's stream by these two events
+  hipStream_t hash_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint32_t* gtab = nullptr;
   uint32_t* qs = nullptr;
   uint32_t grid_max = 0;  // ecmult blocks (qs is sized for grid_max * WG lanes)
@@ -182,8 +191,18 @@ bool split_batch(const DevCtx& d, size_t n) {
 
 // enqueue the verify of n records at d_records; verdict words in out_bits
 // ((n + 31) / 32 words, device memory) or, when null, in d.bits
+// late_join (full-grid batches of standard inputs only): the event after
+// which the records carry their final messages — st waits for it after the
+// ecmult launch, then hkv_late_u1_kernel redoes u1 from them
+// whether a full-grid batch of n runs the 2-wave (mid-size) instance
+bool mid_batch(const DevCtx& d, size_t n) {
+  return !split_batch(d, n) && round_up(n, hkv::WG) <= (size_t)d.grid_max * hkv::WG / 2;
+}
+
+// prologue_done: the caller launched the mid-size lane prologue itself
+// (enqueue_std_chunk's standard-input form)
 int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st,
-                   uint32_t* out_bits = nullptr) {
+                   uint32_t* out_bits = nullptr, hipEvent_t late_join = nullptr, bool prologue_done = false) {
   const size_t n_pad = round_up(n, hkv::WG);
   int rc = ensure_dev_buffers(d, n_pad);
   if (rc) return rc;
@@ -201,15 +220,19 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // (measured: a 115k batch at ~1.8 waves/SIMD took 2.1 ms split vs 1.5 ms
   // unsplit; the bound itself re-measured in profiles/r02_split_threshold.log).
   const bool split = split_batch(d, n);
-  if (!split) HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
+  // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
+  // ecmult instance, every block resident at its 2-wave allocation. (Record
+  // batches keep the three prologue kernels here: the lane-per-signature form
+  // measured 87 against their 75 us on a 115k batch, profiles/r04f; it pays
+  // only inside the overlapped standard-input path.)
+  const bool mid = mid_batch(d, n);
+  if (!split && !prologue_done)
+    HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
   if (split) {
     rc = ensure_aux(d, n_pad, st);
     if (rc) return rc;
   }
   if (d.profile) HKV_TRY(hipEventRecord(e[1], st), "hipEventRecord");
-  // at most 2 waves per SIMD (half the 4-wave resident grid): the paired-form
-  // instance, every block resident at its 2-wave allocation
-  const bool mid = !split && n_pad <= (size_t)d.grid_max * hkv::WG / 2;
   const uint32_t blocks = split ? 0u  // (the small-batch launch sizes its own grid)
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, mid ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
@@ -221,6 +244,10 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // through y_c = num / den (hkv_kernels.hip §2b). The rare-lane count is
   // re-armed by the verdict kernel; a call that failed between the finish
   // and verdict launches leaves it dirty, so it is zeroed on the stream first.
+  if (late_join != nullptr && !split) {
+    HKV_TRY(hipStreamWaitEvent(st, late_join, 0), "hipStreamWaitEvent(hash join)");
+    HKV_TRY(hkv::launch_late_u1(d_records, (uint32_t)n, (uint32_t)n_pad, d.im, st), "late u1 launch");
+  }
   if (!split) {
     if (d.rare_dirty) {
       HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), st), "hipMemset(rare counter)");
@@ -251,6 +278,9 @@ int init_device(DevCtx& d, int device) {
   d.n_cu = prop.multiProcessorCount;
   HKV_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
   HKV_TRY(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking), "hipStreamCreate(copy)");
+  HKV_TRY(hipStreamCreateWithFlags(&d.hash_stream, hipStreamNonBlocking), "hipStreamCreate(hash)");
+  HKV_TRY(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming), "hipEventCreate(fork)");
+  HKV_TRY(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming), "hipEventCreate(join)");
   HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
   HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
   // running sum + finished-workgroup count (the scan re-arms them itself) +
@@ -308,6 +338,9 @@ void free_device(DevCtx& d) {
   if (d.last_use) (void)hipEventDestroy(d.last_use);
   if (d.stream) (void)hipStreamDestroy(d.stream);
   if (d.copy_stream) (void)hipStreamDestroy(d.copy_stream);
+  if (d.hash_stream) (void)hipStreamDestroy(d.hash_stream);
+  if (d.ev_fork) (void)hipEventDestroy(d.ev_fork);
+  if (d.ev_join) (void)hipEventDestroy(d.ev_join);
   d = DevCtx();
 }
 
@@ -430,6 +463,9 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
 // P2SH / P2WSH / P2SH-P2WSH): the scan (inside the block kernel, or
 // hkv_ms_scan_kernel) leaves the batch total on the device and the tail
 // kernel (hkv_kernels.hip 2e) does the rest, or nothing when the total is 0.
+int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
+                     uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
+                     bool lane_prologue, const hkv::MsScan& ms, size_t cap_cand);
 int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                       uint32_t* out_bits, hipStream_t st) {
   const bool fused = split_batch(d, n);
@@ -456,15 +492,73 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   d.ms_dirty = true;  // until this call's tail is enqueued
   uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr);
   const hkv::MsScan ms{desc, off, ctr};
-  rc = fused ? enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE) : enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
-  if (!rc && fused) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, fused_scan ? &ms : nullptr, st);
-  if (rc) return rc;
-  if (!fused_scan)
+  // Larger batches (HKV_STD_OVERLAP): the index rows and the parse half on
+  // st, then the hash half (BIP143 per-tx hashes, the script checks and the
+  // sighashes, rewriting each record whole) on the hash stream while st runs
+  // the multisig scan, the prologue and the Q chains, which need only r, s
+  // and the key; st joins before u1 (hkv_late_u1_kernel) and the finish.
+  const bool overlap = !fused && HKV_STD_OVERLAP;
+  const bool lane_prologue = overlap && mid_batch(d, n);
+  bool forked = false;
+  if (fused) {
+    rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
+    if (!rc) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, fused_scan ? &ms : nullptr, st);
+  } else if (overlap) {
+    rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
+    if (rc) return rc;
+    if (lane_prologue)  // the parse half inside the mid-size lane prologue
+      HKV_TRY(hkv::launch_std_lane_prologue(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs,
+                                            (uint32_t)n, (uint32_t)round_up(n, hkv::WG), forkid,
+                                            static_cast<uint8_t*>(recs), d.im, st),
+              "std lane prologue launch");
+    else
+      HKV_TRY(hkv::launch_std_parse(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
+                                    forkid, static_cast<uint8_t*>(recs), st),
+              "std parse launch");
+    HKV_TRY(hipEventRecord(d.ev_fork, st), "hipEventRecord(fork)");
+    HKV_TRY(hipStreamWaitEvent(d.hash_stream, d.ev_fork, 0), "hipStreamWaitEvent(fork)");
+    forked = true;
+    hipError_t e = hkv::launch_tx_hashes_only(dt->bytes, dt->offsets, dt->n_tx, std_tx_hashes(forkid), d.txt,
+                                              d.hash_stream);
+    if (e == hipSuccess)
+      e = hkv::launch_std_inputs(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
+                                 static_cast<uint8_t*>(recs), d.hash_stream);
+    // the multisig scan needs only the index rows: off st's path too
+    if (e == hipSuccess && !fused_scan)
+      e = hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
+                              desc, off, ctr, d.hash_stream);
+    // (recorded whatever happened: an error below still joins st to it)
+    const hipError_t e2 = hipEventRecord(d.ev_join, d.hash_stream);
+    if (e != hipSuccess) rc = hip_fail(e, "std hash half launch");
+    else if (e2 != hipSuccess) rc = hip_fail(e2, "hipEventRecord(join)");
+  } else {
+    rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
+  }
+  if (!rc)
+    rc = enqueue_std_rest(d, dt, jobs, n, forkid, recs, out_bits, st, fused, fused_scan, overlap, lane_prologue, ms,
+                          cap_cand);
+  // a failed call still orders st after the hash half (the next call's
+  // scratch acquire then waits for it too)
+  if (rc && forked) (void)hipStreamWaitEvent(st, d.ev_join, 0);
+  if (!rc) d.ms_dirty = false;
+  return rc;
+}
+
+// the rest of enqueue_std_chunk after the extraction launches: the
+// multisig scan, the record verify, the multisig tail
+int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
+                     uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
+                     bool lane_prologue, const hkv::MsScan& ms, size_t cap_cand) {
+  uint32_t* desc = ms.desc;
+  uint64_t* off = ms.off;
+  uint64_t* ctr = ms.counters;
+  int rc = HKV_OK;
+  if (!fused_scan && !overlap)  // (the overlapped form scanned on the hash stream)
     HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
                                 desc, off, ctr, st),
             "multisig scan launch");
   if (!fused) {
-    rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits);
+    rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits, overlap ? d.ev_join : nullptr, lane_prologue);
     if (rc) return rc;
   }
   uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
@@ -495,7 +589,6 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   t.out_bits = out_bits;
   t.bar = d.ms_bar;
   HKV_TRY(hkv::launch_ms_tail(t, (uint32_t)d.n_cu, st), "multisig tail launch");
-  d.ms_dirty = false;
   return HKV_OK;
 }
 

@@ -80,6 +80,15 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
                                    uint32_t n_cu, const MsScan* ms, hipStream_t st);
 bool std_split_scans(uint32_t n_pad, uint32_t n_cu);
 // y-free full-grid batches: u1 * G, the y0 = num / den reduction and the verdict bitmap
+// mid-size standard-input batches (the overlapped path): std_parse, prologue,
+// s^-1 and GLV in one lane-per-input launch that writes each input's record
+// with a zero message (the hash half completes them)
+hipError_t launch_std_lane_prologue(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
+                                    int32_t forkid, uint8_t* recs, uint32_t* im, hipStream_t st);
+// u1 = m / s and its G digits from the final records (after the overlapped
+// extraction's hash half): a record the hash half zeroed loses FLAG_VALID
+hipError_t launch_late_u1(const void* recs, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st);
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
                          uint32_t* bits, uint32_t n_words, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
@@ -101,6 +110,14 @@ hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt
 hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                              uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                              uint8_t* recs, hipStream_t st);
+// the overlapped extraction of large batches: the parse half alone (records
+// without the message) and the BIP143 per-tx hashes alone (rows written by
+// launch_tx_index(TX_HASHES_NONE) before)
+hipError_t launch_std_parse(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                            uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid, uint8_t* recs,
+                            hipStream_t st);
+hipError_t launch_tx_hashes_only(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t hashes,
+                                 uint32_t* txt, hipStream_t st);
 // multisig inputs: the scan (hkv_sighash.hip section 4; the tail in hkv_kernels.hip)
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,

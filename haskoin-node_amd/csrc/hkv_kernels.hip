@@ -369,6 +369,35 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
   glv_lane(im, n_pad, i, flags, sinv);
 }
 
+// 1c'. large standard-input batches (hkv_api.cpp enqueue_std_chunk): the
+//      prologue ran on records whose message the hash half was still writing,
+//      so the G digits are redone here from the final record, after the
+//      join: m = msg mod n, u1 = m s^-1 (IM_C still holds s^-1: the ecmult
+//      kernel writes B' over the Q digits only). A record the hash half
+//      zeroed (a failed HASH160 / script check) makes the lane invalid.
+__global__ void __launch_bounds__(WG) hkv_late_u1_kernel(const uint32_t* __restrict__ recs, uint32_t n,
+                                                         uint32_t n_pad, uint32_t* __restrict__ im) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* w = recs + (size_t)i * REC_WORDS;
+  uint32_t f = im[(size_t)IM_FLAGS * n_pad + i];
+  if ((w[24] & 0xFFu) == 0u && (f & FLAG_VALID)) {
+    f &= ~FLAG_VALID;
+    im[(size_t)IM_FLAGS * n_pad + i] = f;
+  }
+  const bool use = (f & FLAG_VALID) != 0;
+  sc m, sinv, u1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m.v[7 - j] = __builtin_bswap32(w[j]);
+  sc_cond_sub_n(m.v);
+  im_load8(im, n_pad, IM_C, i, sinv.v);
+  sc_mul(u1, m, sinv);
+  uint32_t SL[4], SH[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
+  write_gdigits(im, n_pad, i, SL, SH);
+}
+
 // ---------------------------------------------------------------------------
 // 1d. small batches (the split ecmult's range, e.g. one block): no separate
 //     prologue launch; waves 4-5 of each split-ecmult workgroup parse the
@@ -906,6 +935,45 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
   flags = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
   im[(size_t)IM_FLAGS * n_pad + i] = flags;
 }
+// 1e. Mid-size standard-input batches (at most 2 waves per SIMD; the
+//     overlapped path of hkv_api.cpp enqueue_std_chunk): std_parse
+//     (verifyStdInput's parse half), the prologue, s^-1 and the GLV split in
+//     one lane per input (sig_lane_q / sig_lane_g: a per-lane variable-time
+//     safegcd instead of the batch trick). The lane writes the input's record
+//     with a zero message — the hash half (hkv_std_input_kernel, on a second
+//     stream) rewrites it whole and hkv_late_u1_kernel redoes u1 after the
+//     join; s^-1 stays in IM_C for it.
+__global__ void __launch_bounds__(WG) hkv_std_lane_prologue_kernel(uint32_t* __restrict__ recs, uint32_t n,
+                                                                   uint32_t n_pad, uint32_t* __restrict__ im,
+                                                                   StdArgs sa) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n_pad) return;
+  bool glv_ok, n1, n2;
+  uint32_t kw[REC_WORDS];
+  StdIn x = {};
+  key_words_of<true>(i, n, recs, sa, kw, x);
+  sc r, s, m, sinv;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { r.v[k] = x.r[k]; s.v[k] = x.s[k]; m.v[k] = 0; }
+  bool ok = i < n && x.ok;
+  sig_lane_q(r, s, HKV_MODE_HASKOIN, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
+  sig_lane_g(m, sinv, ok && glv_ok, im, n_pad, i);
+  fe kx, kwv;
+  uint32_t pflags = 0;
+  const bool pk = pubkey_parse_rec_w(kw, kx, kwv, pflags) && i < n;
+  im[(size_t)IM_FLAGS * n_pad + i] = split_flags(ok, (pk ? 1u : 0u) | pflags, glv_ok, n1, n2);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    im[(size_t)(IM_QX + k) * n_pad + i] = kx.v[k];
+    im[(size_t)(IM_W + k) * n_pad + i] = kwv.v[k];
+    im[(size_t)(IM_C + k) * n_pad + i] = sinv.v[k];
+  }
+  if (i < n) {
+    const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    std_write_record(recs + (size_t)i * REC_WORDS, x, true, zero);
+  }
+}
+
 // The signature wave, second half (whole wave: the STD hashes are
 // block-synchronous): STD — the script checks, the sighash and the input's
 // verify record; then u1 = m / s and A = u1 G into aux.
@@ -2295,6 +2363,19 @@ hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st) {
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
   hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div((size_t)GTAB_TABLES * GTAB_ENTRIES, WG)), dim3(WG), 0, st,
                      gtab);
+  return hipGetLastError();
+}
+hipError_t launch_std_lane_prologue(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
+                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
+                                    int32_t forkid, uint8_t* recs, uint32_t* im, hipStream_t st) {
+  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(hkv_std_lane_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st,
+                     reinterpret_cast<uint32_t*>(recs), n, n_pad, im, sa);
+  return hipGetLastError();
+}
+hipError_t launch_late_u1(const void* recs, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(hkv_late_u1_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, (const uint32_t*)recs, n, n_pad, im);
   return hipGetLastError();
 }
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
