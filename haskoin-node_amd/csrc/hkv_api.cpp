@@ -24,6 +24,9 @@
 #ifndef HKV_STD_OVERLAP
 #define HKV_STD_OVERLAP 1
 #endif
+#ifndef HKV_STD_FUSED_PROLOGUE
+#define HKV_STD_FUSED_PROLOGUE 1
+#endif
 
 namespace {
 
@@ -64,7 +67,7 @@ struct DevCtx {
   // records, [5] key-check verdict words, [6] host-form verdict words
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
-  void* ms_ctr = nullptr;            // scan counters: [0] running sum, [1] finished groups, [2] published total
+  void* ms_ctr = nullptr;            // scan counters: [0] running sum (the tail reads and re-arms it)
   unsigned int* ms_bar = nullptr;    // the tail kernel's grid barrier: [0] arrivals, [1] sense, [2] fault
   bool ms_dirty = false;             // a call failed after its scan launch: zero ms_ctr before the next scan
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
@@ -199,10 +202,13 @@ bool mid_batch(const DevCtx& d, size_t n) {
   return !split_batch(d, n) && round_up(n, hkv::WG) <= (size_t)d.grid_max * hkv::WG / 2;
 }
 
-// prologue_done: the caller launched the mid-size lane prologue itself
-// (enqueue_std_chunk's standard-input form)
+// std_pro (mid-size standard-input batches, enqueue_std_chunk): the signature
+// and key come from the batch's txs through the lane prologue — at the head of
+// the ecmult kernel (HKV_STD_FUSED_PROLOGUE) or as a launch before it —
+// instead of from records
 int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st,
-                   uint32_t* out_bits = nullptr, hipEvent_t late_join = nullptr, bool prologue_done = false) {
+                   uint32_t* out_bits = nullptr, hipEvent_t late_join = nullptr,
+                   const hkv::StdOps* std_pro = nullptr) {
   const size_t n_pad = round_up(n, hkv::WG);
   int rc = ensure_dev_buffers(d, n_pad);
   if (rc) return rc;
@@ -226,8 +232,11 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // measured 87 against their 75 us on a 115k batch, profiles/r04f; it pays
   // only inside the overlapped standard-input path.)
   const bool mid = mid_batch(d, n);
-  if (!split && !prologue_done)
+  if (std_pro != nullptr && !mid) return HKV_E_INTERNAL;  // (the lane prologue is a mid-size form)
+  if (!split && std_pro == nullptr)
     HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
+  if (std_pro != nullptr && !HKV_STD_FUSED_PROLOGUE)
+    HKV_TRY(hkv::launch_std_lane_prologue(*std_pro, (uint32_t)n, (uint32_t)n_pad, d.im, st), "lane prologue launch");
   if (split) {
     rc = ensure_aux(d, n_pad, st);
     if (rc) return rc;
@@ -237,9 +246,14 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, mid ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
-  HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, mid,
-                             d.profile ? d.clk : nullptr, d.aux, d_records, mode, (uint32_t)d.n_cu, st),
-          "ecmult launch");
+  if (std_pro != nullptr && HKV_STD_FUSED_PROLOGUE)
+    HKV_TRY(hkv::launch_std_ecmult_mid(*std_pro, d.im, (uint32_t)n, (uint32_t)n_pad, d.qs, blocks,
+                                       d.profile ? d.clk : nullptr, st),
+            "ecmult launch");
+  else
+    HKV_TRY(hkv::launch_ecmult(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.qs, blocks, vbits, n_words, split, mid,
+                               d.profile ? d.clk : nullptr, d.aux, d_records, mode, (uint32_t)d.n_cu, st),
+            "ecmult launch");
   // full-grid batches: the finish kernels add u1 * G and decide x(R) == r
   // through y_c = num / den (hkv_kernels.hip §2b). The rare-lane count is
   // re-armed by the verdict kernel; a call that failed between the finish
@@ -283,8 +297,8 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming), "hipEventCreate(join)");
   HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
   HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
-  // running sum + finished-workgroup count (the scan re-arms them itself) +
-  // the published total the multisig tail reads; the tail's barrier words
+  // the multisig scan's running sum (the tail kernel reads and re-arms it);
+  // the tail's barrier words
   HKV_TRY(hipMalloc(&d.ms_ctr, 4 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 4 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
   HKV_TRY(hipMalloc(reinterpret_cast<void**>(&d.ms_bar), 4 * sizeof(unsigned int)), "hipMalloc(multisig barrier)");
@@ -492,11 +506,12 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   d.ms_dirty = true;  // until this call's tail is enqueued
   uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr);
   const hkv::MsScan ms{desc, off, ctr};
-  // Larger batches (HKV_STD_OVERLAP): the index rows and the parse half on
-  // st, then the hash half (BIP143 per-tx hashes, the script checks and the
-  // sighashes, rewriting each record whole) on the hash stream while st runs
-  // the multisig scan, the prologue and the Q chains, which need only r, s
-  // and the key; st joins before u1 (hkv_late_u1_kernel) and the finish.
+  // Larger batches (HKV_STD_OVERLAP): the index rows on st, then the hash
+  // half (BIP143 per-tx hashes, the script checks and the sighashes, writing
+  // each record whole; the multisig scan) on the hash stream while st runs
+  // the parse half, the prologue and the Q chains, which need only r, s and
+  // the key — at mid size all inside the ecmult launch (kernel 1e); st joins
+  // before u1 (hkv_late_u1_kernel) and the finish.
   const bool overlap = !fused && HKV_STD_OVERLAP;
   const bool lane_prologue = overlap && mid_batch(d, n);
   bool forked = false;
@@ -506,12 +521,10 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   } else if (overlap) {
     rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
     if (rc) return rc;
-    if (lane_prologue)  // the parse half inside the mid-size lane prologue
-      HKV_TRY(hkv::launch_std_lane_prologue(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs,
-                                            (uint32_t)n, (uint32_t)round_up(n, hkv::WG), forkid,
-                                            static_cast<uint8_t*>(recs), d.im, st),
-              "std lane prologue launch");
-    else
+    // (mid-size batches: the parse half runs inside the lane prologue, which
+    // writes no record — the hash half writes each record whole — so the
+    // fork comes right after the index rows)
+    if (!lane_prologue)
       HKV_TRY(hkv::launch_std_parse(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
                                     forkid, static_cast<uint8_t*>(recs), st),
               "std parse launch");
@@ -558,7 +571,9 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
                                 desc, off, ctr, st),
             "multisig scan launch");
   if (!fused) {
-    rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits, overlap ? d.ev_join : nullptr, lane_prologue);
+    const hkv::StdOps so{dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, forkid};
+    rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits, overlap ? d.ev_join : nullptr,
+                        lane_prologue ? &so : nullptr);
     if (rc) return rc;
   }
   uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
@@ -577,7 +592,7 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
   t.hash_txs = fused ? std_tx_hashes(forkid) : hkv::TX_HASHES_NONE;
   t.desc = desc;
   t.off = off;
-  t.total = reinterpret_cast<const unsigned long long*>(ctr + 2);
+  t.total = reinterpret_cast<unsigned long long*>(ctr);
   t.cand = cand;
   t.keyrec = cand + cap_cand * hkv::REC_SIZE;
   t.cbits = static_cast<uint32_t*>(d.ms[3]);

@@ -33,7 +33,8 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 // the multisig scan operands a fused launch may take over (hkv_ms_scan_kernel's);
-// counters: [0] running sum, [1] finished groups, [2] the published total
+// counters: [0] the running sum (candidates | key checks << 32), which the tail
+// kernel reads after the scan and re-arms
 struct MsScan {
   uint32_t* desc;
   uint64_t* off;
@@ -57,7 +58,7 @@ struct MsTail {
   uint32_t hash_txs;  // TX_HASHES_* the tail computes first (the fused path's index hashed nothing)
   const uint32_t* desc;
   const uint64_t* off;
-  const unsigned long long* total;  // MsScan counters + 2
+  unsigned long long* total;        // MsScan counters[0]: the scan's running sum (the tail re-arms it)
   uint8_t* cand;                    // candidate records (capacity n * 136)
   uint8_t* keyrec;                  // key-check records (capacity n * 16)
   uint32_t* cbits;                  // candidate verdict words
@@ -80,12 +81,22 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
                                    uint32_t n_cu, const MsScan* ms, hipStream_t st);
 bool std_split_scans(uint32_t n_pad, uint32_t n_cu);
 // y-free full-grid batches: u1 * G, the y0 = num / den reduction and the verdict bitmap
+// the operands of a standard-input batch (txs, index rows, prevout scripts, jobs)
+struct StdOps {
+  const uint8_t* txs;
+  uint32_t n_tx;
+  const uint32_t* txt;
+  const uint8_t* scripts;
+  uint32_t scripts_len;
+  const hkv_input_job* jobs;
+  int32_t forkid;
+};
 // mid-size standard-input batches (the overlapped path): std_parse, prologue,
-// s^-1 and GLV in one lane-per-input launch that writes each input's record
-// with a zero message (the hash half completes them)
-hipError_t launch_std_lane_prologue(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
-                                    int32_t forkid, uint8_t* recs, uint32_t* im, hipStream_t st);
+// s^-1 and GLV in one lane per input — a launch of its own, or at the head of
+// the mid-size ecmult kernel's lanes (launch_std_ecmult_mid)
+hipError_t launch_std_lane_prologue(const StdOps& o, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st);
+hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint32_t n_pad, uint32_t* qs,
+                                 uint32_t grid, unsigned long long* clk, hipStream_t st);
 // u1 = m / s and its G digits from the final records (after the overlapped
 // extraction's hash half): a record the hash half zeroed loses FLAG_VALID
 hipError_t launch_late_u1(const void* recs, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st);

@@ -457,6 +457,24 @@ HKV_DEV uint32_t split_flags(bool ok, uint32_t pk_ok, bool glv_ok, bool n1, bool
   return f;
 }
 
+struct StdArgs {
+  const uint8_t* txs;
+  uint32_t n_tx;
+  const uint32_t* txt;
+  const uint8_t* scripts;
+  uint32_t scripts_len;
+  const hkv_input_job* jobs;
+  int32_t forkid;
+  // the multisig scan the block kernel runs on its square-root wave
+  // (hkv_ms_scan_kernel's operands; null: the host launches the scan)
+  uint32_t* ms_desc;
+  uint64_t* ms_off;
+  unsigned long long* ms_ctr;
+};
+// the standard-input lane prologue (1e) run at the head of the mid-size
+// ecmult kernel's lane (defined below, after the std parse helpers)
+HKV_DEV void std_lane_prologue(uint32_t i, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im, const StdArgs& sa);
+
 // ---------------------------------------------------------------------------
 // 2. ecmult + x compare
 // ---------------------------------------------------------------------------
@@ -499,11 +517,16 @@ HKV_DEV bool x_matches_r(const fe& Xin, const fe& Z, const uint32_t r[8]);
 // instance, which is allocated for 2 waves per SIMD (no spill). The 1M
 // launch keeps the plain forms: its 4 waves per SIMD already fill the issue
 // slots.
-template <bool ILP>
+// STDPRO (mid-size standard-input batches): each lane first runs the
+// standard-input lane prologue (1e: std_parse, s^-1, GLV, digits into im)
+// for its input, so the latency-bound prologue phase runs inside this launch's
+// occupancy instead of as a launch of its own before it.
+template <bool ILP, bool STDPRO = false>
 __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_kernel(uint32_t* __restrict__ im,
                                                                                  uint32_t n, uint32_t n_pad,
                                                                                  uint32_t* __restrict__ qs,
-                                                                                 unsigned long long* __restrict__ clk) {
+                                                                                 unsigned long long* __restrict__ clk,
+                                                                                 StdArgs sa) {
   const uint32_t n_lanes = gridDim.x * WG;
   const uint32_t lane = blockIdx.x * WG + threadIdx.x;
   // optional clock probe (hkv_profile_clock): shader-clock and constant-rate
@@ -516,6 +539,7 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
 
   for (uint32_t base = blockIdx.x * WG; base < n_pad; base += gridDim.x * WG) {
     const uint32_t i = base + threadIdx.x;
+    if constexpr (STDPRO) std_lane_prologue(i, n, n_pad, im, sa);  // (read back below by the same lane)
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
     ge q;
@@ -708,20 +732,6 @@ HKV_DEV void std_key_words(uint32_t kw[REC_WORDS], const StdIn& x) {
   }
 }
 // the standard-input operands (hkv_verify_std_inputs*)
-struct StdArgs {
-  const uint8_t* txs;
-  uint32_t n_tx;
-  const uint32_t* txt;
-  const uint8_t* scripts;
-  uint32_t scripts_len;
-  const hkv_input_job* jobs;
-  int32_t forkid;
-  // the multisig scan the block kernel runs on its square-root wave
-  // (hkv_ms_scan_kernel's operands; null: the host launches the scan)
-  uint32_t* ms_desc;
-  uint64_t* ms_off;
-  unsigned long long* ms_ctr;
-};
 
 // Pair-form pieces shared by the small-batch kernels (2c, 2d). Each chain
 // lane keeps its own coordinate of every table entry in LDS: ql is one chain
@@ -939,19 +949,17 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
 //     overlapped path of hkv_api.cpp enqueue_std_chunk): std_parse
 //     (verifyStdInput's parse half), the prologue, s^-1 and the GLV split in
 //     one lane per input (sig_lane_q / sig_lane_g: a per-lane variable-time
-//     safegcd instead of the batch trick). The lane writes the input's record
-//     with a zero message — the hash half (hkv_std_input_kernel, on a second
-//     stream) rewrites it whole and hkv_late_u1_kernel redoes u1 after the
-//     join; s^-1 stays in IM_C for it.
-__global__ void __launch_bounds__(WG) hkv_std_lane_prologue_kernel(uint32_t* __restrict__ recs, uint32_t n,
-                                                                   uint32_t n_pad, uint32_t* __restrict__ im,
-                                                                   StdArgs sa) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n_pad) return;
+//     safegcd instead of the batch trick) — at the head of the mid-size ecmult
+//     kernel (STDPRO) or, with HKV_STD_FUSED_PROLOGUE=0, as a launch of its
+//     own. Nothing here writes the input's record: the hash half
+//     (hkv_std_input_kernel, on a second stream from the start) writes it
+//     whole, and hkv_late_u1_kernel redoes u1 from it after the join; s^-1
+//     stays in IM_C for that.
+HKV_DEV void std_lane_prologue(uint32_t i, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im, const StdArgs& sa) {
   bool glv_ok, n1, n2;
   uint32_t kw[REC_WORDS];
   StdIn x = {};
-  key_words_of<true>(i, n, recs, sa, kw, x);
+  key_words_of<true>(i, n, nullptr, sa, kw, x);
   sc r, s, m, sinv;
 #pragma unroll
   for (int k = 0; k < 8; ++k) { r.v[k] = x.r[k]; s.v[k] = x.s[k]; m.v[k] = 0; }
@@ -968,10 +976,11 @@ __global__ void __launch_bounds__(WG) hkv_std_lane_prologue_kernel(uint32_t* __r
     im[(size_t)(IM_W + k) * n_pad + i] = kwv.v[k];
     im[(size_t)(IM_C + k) * n_pad + i] = sinv.v[k];
   }
-  if (i < n) {
-    const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    std_write_record(recs + (size_t)i * REC_WORDS, x, true, zero);
-  }
+}
+__global__ void __launch_bounds__(WG) hkv_std_lane_prologue_kernel(uint32_t n, uint32_t n_pad,
+                                                                   uint32_t* __restrict__ im, StdArgs sa) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i < n_pad) std_lane_prologue(i, n, n_pad, im, sa);
 }
 
 // The signature wave, second half (whole wave: the STD hashes are
@@ -1456,12 +1465,6 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       }
     }
     __syncthreads();  // the group's LDS (tables, exchanges, flags' data) is read before the next group's writes
-  }
-  if constexpr (STD) {  // the last workgroup publishes the batch's multisig record count
-    if (wv == 2 && sa.ms_desc != nullptr) {
-      __threadfence();
-      if (ln == 0) ms_scan_done(sa.ms_ctr, gridDim.x);
-    }
   }
 }
 
@@ -2238,10 +2241,16 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t buf[16 * PAIR_TPB];  // sha256_stream blocks ([word][thread])
   __shared__ uint32_t okf;
+  // the scan's running sum (final: the scan ran before this launch on the
+  // stream); every workgroup reads it before its first grid barrier, and
+  // workgroup 0 re-arms it after that barrier (or on a barrier fault)
   const unsigned long long total = __hip_atomic_load(a.total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
-  if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid
+  if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid, nothing to re-arm
   unsigned int sense = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto rearm = [&]() {
+    if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   const uint32_t tid = blockIdx.x * PAIR_TPB + threadIdx.x, nthr = gridDim.x * PAIR_TPB;
   // 1. the BIP143 per-tx hashes (lanes: hash-major, so a wave mostly shares its hash)
   if (a.hash_txs != TX_HASHES_NONE && a.n_tx) {
@@ -2254,7 +2263,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
       if (go && a.hash_txs == TX_HASHES_WITNESS) go = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
       tx_hash_word_lane(a.txs, row, which, go, buf);
     }
-    if (!grid_sync(a.bar, sense, &okf)) return;
+    if (!grid_sync(a.bar, sense, &okf)) return rearm();
   }
   // 2. key-check and candidate records
   for (uint32_t b = 0; b < a.n; b += nthr) {
@@ -2262,7 +2271,8 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
     ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
                  a.cand, a.keyrec, buf);
   }
-  if (!grid_sync(a.bar, sense, &okf)) return;
+  if (!grid_sync(a.bar, sense, &okf)) return rearm();
+  rearm();  // (every workgroup has read the total)
   // 3. key checks, then the candidates in pair-form groups of 32
   for (uint32_t b = 0; b < n_keys; b += nthr)
     key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), b + tid, n_keys, a.kbits);
@@ -2275,7 +2285,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
                       reinterpret_cast<uint32_t*>(a.cand) + (size_t)shift * REC_WORDS, HKV_MODE_HASKOIN, nullptr,
                       none, qlds, hlds, xch, buf);
   }
-  if (!grid_sync(a.bar, sense, &okf)) return;
+  if (!grid_sync(a.bar, sense, &okf)) return rearm();
   // 4. the countMulSig walk
   for (uint32_t b = 0; b < a.n; b += nthr) {
     const uint32_t jx = b + tid;
@@ -2327,9 +2337,11 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
     hipLaunchKernelGGL(hkv_pair_split_kernel<false>, dim3(n_pad / PAIR_SIGS), dim3(PAIR_TPB), 0, st, im, n, n_pad,
                        gtab, bits, n_words, aux, rw, mode, clk, StdArgs{});  // (record batches: no std operands)
   else if (mid)
-    hipLaunchKernelGGL(hkv_ecmult_kernel<true>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
+    hipLaunchKernelGGL((hkv_ecmult_kernel<true, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk,
+                       StdArgs{});
   else
-    hipLaunchKernelGGL(hkv_ecmult_kernel<false>, dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk);
+    hipLaunchKernelGGL((hkv_ecmult_kernel<false, false>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk,
+                       StdArgs{});
   return hipGetLastError();
 }
 // small batches of standard inputs: parse, the Q chains, the script checks,
@@ -2365,12 +2377,18 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
                      gtab);
   return hipGetLastError();
 }
-hipError_t launch_std_lane_prologue(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
-                                    int32_t forkid, uint8_t* recs, uint32_t* im, hipStream_t st) {
-  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(hkv_std_lane_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st,
-                     reinterpret_cast<uint32_t*>(recs), n, n_pad, im, sa);
+static StdArgs std_args(const StdOps& o) {
+  return StdArgs{o.txs, o.n_tx, o.txt, o.scripts, o.scripts_len, o.jobs, o.forkid, nullptr, nullptr, nullptr};
+}
+hipError_t launch_std_lane_prologue(const StdOps& o, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_std_lane_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n, n_pad, im,
+                     std_args(o));
+  return hipGetLastError();
+}
+hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint32_t n_pad, uint32_t* qs,
+                                 uint32_t grid, unsigned long long* clk, hipStream_t st) {
+  hipLaunchKernelGGL((hkv_ecmult_kernel<true, true>), dim3(grid), dim3(WG), 0, st, im, n, n_pad, qs, clk,
+                     std_args(o));
   return hipGetLastError();
 }
 hipError_t launch_late_u1(const void* recs, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st) {

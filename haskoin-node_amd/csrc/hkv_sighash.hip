@@ -204,9 +204,6 @@ __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restri
   __shared__ uint32_t buf[16 * WG];
   const uint32_t jx = blockIdx.x * WG + threadIdx.x;
   ms_scan_lane(txs, n_tx, txt, scripts, scripts_len, jobs, jx, jx < n, forkid, desc, off, counters, buf);
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) ms_scan_done(counters, gridDim.x);
 }
 
 }  // namespace hkv
@@ -267,8 +264,9 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
 // ---------------------------------------------------------------------------
 namespace hkv {
 
-// per-input desc words and record offsets; counters[2] ends as the number of
-// candidate records | key-check records << 32 (ms_scan_done)
+// per-input desc words and record offsets; counters[0] ends as the number of
+// candidate records | key-check records << 32 (the tail kernel reads it,
+// stream-ordered after the scan, and re-arms it)
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                           uint32_t* desc, uint64_t* off, uint64_t* counters, hipStream_t st) {

@@ -1352,23 +1352,6 @@ HKV_DEV void ms_scan_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const 
     off[jx] = ok ? (uint64_t)atomicAdd(total, (unsigned long long)r.n_cand | ((unsigned long long)r.n << 32)) : 0ull;
   }
 }
-// One thread per finished group of scanned inputs, after a device fence:
-// the last of n_groups moves the sum to counters[2] (where the multisig tail
-// kernel reads it: candidates | key checks << 32) and re-arms the running
-// counters (counters[0] the sum, counters[1] the finished-group count), so
-// the stream carries no memset, no D2H copy and the host waits for nothing.
-HKV_DEV void ms_scan_done(unsigned long long* counters, uint32_t n_groups) {
-  unsigned long long* total = counters;
-  unsigned int* done = reinterpret_cast<unsigned int*>(counters + 1);
-  if (atomicAdd(done, 1u) == n_groups - 1) {
-    __threadfence();
-    const unsigned long long t = atomicExch(total, 0ull);
-    atomicExch(done, 0u);
-    atomicExch(counters + 2, t);
-    __threadfence();
-  }
-}
-
 // record: msg32 (digest byte order words) | r | s (limbs, written big-endian) |
 // pklen | pubkey | zero padding
 HKV_DEV void ms_write_record(uint32_t* r32, const uint32_t msg[8], const uint32_t r[8], const uint32_t s[8],

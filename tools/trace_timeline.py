@@ -14,7 +14,7 @@ import sys
 def main(path: str) -> None:
     rows = [r for r in csv.DictReader(open(path)) if "hkv" in r["Kernel_Name"] and "gen_" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ec = [i for i, r in enumerate(rows) if "ecmult_kernel<true>" in r["Kernel_Name"]]
+    ec = [i for i, r in enumerate(rows) if "ecmult_kernel<true" in r["Kernel_Name"]]
     i = ec[-1]
     j = i  # back to the call's tx index / tx hash launch
     while j > 0 and not ("tx_hash" in rows[j]["Kernel_Name"] or "tx_index" in rows[j]["Kernel_Name"]):
