@@ -257,7 +257,9 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
                              "enqueue_us_per_block": round(t_enq / 32 * 1e6, 1),
                              "note": "32 calls of hkv_verify_std_inputs_device on one stream, no host sync between "
                                      "them; host wall clock from the first enqueue to the last verdict"}
-    res["split_phases_us"] = split_phases(v, torch, run)
+    # (a block: one workgroup of the block kernel per 16 inputs)
+    n_pad = (db.n + 255) // 256 * 256
+    res["split_phases_us"] = split_phases(v, torch, run, n_pad // 16 if n_pad <= 16 * 256 else 0)
     return res, got
 
 
@@ -268,7 +270,7 @@ PHASES = ("start", "lo_table", "digits", "lo_chain", "a_y0", "verdict", "sig_par
           "hi_table", "hi_chain", "mid_chain")
 
 
-def split_phases(v, torch, run) -> dict:
+def split_phases(v, torch, run, n_groups: int = 0) -> dict:
     """Phase boundaries of workgroup 0 of the small-batch kernel in one extra
     profiled call (hkv_profile_phases: constant-rate clock stamps,
     microseconds after the kernel's start)."""
@@ -278,8 +280,22 @@ def split_phases(v, torch, run) -> dict:
     stamps = (ctypes.c_uint64 * len(PHASES))()
     tick = ctypes.c_double()
     v.lib.hkv_profile_phases(v.ctx, 0, stamps, len(PHASES), ctypes.byref(tick))
+    out = {name: round((int(stamps[k]) - int(stamps[0])) * tick.value * 1e-3, 1) for k, name in enumerate(PHASES)}
+    # every workgroup's (start, end) stamps (the block kernel only): how far
+    # the launch's span reaches beyond workgroup 0's phase stamps
+    if n_groups:
+        g = (ctypes.c_uint64 * (2 * n_groups))()
+        v.lib.hkv_profile_group_stamps(v.ctx, 0, g, n_groups, ctypes.byref(tick))
+        st_, en = [int(g[2 * k]) for k in range(n_groups)], [int(g[2 * k + 1]) for k in range(n_groups)]
+        t0, us = min(st_), tick.value * 1e-3
+        ends = sorted((e - t0) * us for e in en)
+        out["groups"] = {"n": n_groups, "start_spread_us": round((max(st_) - t0) * us, 1),
+                         "group0_start_us": round((st_[0] - t0) * us, 1),
+                         "group0_end_us": round((en[0] - t0) * us, 1),
+                         "end_min_us": round(ends[0], 1), "end_median_us": round(ends[len(ends) // 2], 1),
+                         "end_max_us": round(ends[-1], 1)}
     v.lib.hkv_profile_enable(v.ctx, 0)
-    return {name: round((int(stamps[k]) - int(stamps[0])) * tick.value * 1e-3, 1) for k, name in enumerate(PHASES)}
+    return out
 
 
 def block_mix(v, torch, steps: int) -> dict:

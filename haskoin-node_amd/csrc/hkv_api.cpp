@@ -32,6 +32,10 @@ namespace {
 
 thread_local std::string g_last_hip;
 
+// the clock probe: 4 clock counters, 12 phase stamps, then a (start, end)
+// stamp pair per workgroup of the block kernel (hkv_profile_group_stamps)
+constexpr size_t CLK_GROUPS = 4096, CLK_WORDS = 16 + 2 * CLK_GROUPS;
+
 struct DevCtx {
   int device = -1;
   int n_cu = 0;
@@ -307,8 +311,8 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
   HKV_TRY(hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device), "wall clock rate");
-  HKV_TRY(hipMalloc(&d.clk, 16 * sizeof(unsigned long long)), "hipMalloc(clock probe)");
-  HKV_TRY(hipMemsetAsync(d.clk, 0, 16 * sizeof(unsigned long long), d.stream), "hipMemset(clock probe)");
+  HKV_TRY(hipMalloc(&d.clk, CLK_WORDS * sizeof(unsigned long long)), "hipMalloc(clock probe)");
+  HKV_TRY(hipMemsetAsync(d.clk, 0, CLK_WORDS * sizeof(unsigned long long), d.stream), "hipMemset(clock probe)");
   HKV_TRY(hipMalloc(&d.gtab, hkv::GTAB_DWORDS * sizeof(uint32_t)), "hipMalloc(gtab)");  // 448 MiB at radix 2^20
   int per_cu = 0;
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
@@ -1003,6 +1007,19 @@ int hkv_profile_phases(hkv_ctx* ctx, int dev, uint64_t* stamps, size_t n, double
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   HKV_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
   if (n) HKV_TRY(hipMemcpy(stamps, d.clk + 4, n * sizeof(uint64_t), hipMemcpyDeviceToHost), "D2H phase stamps");
+  *tick_ns = d.wall_khz > 0 ? 1e6 / d.wall_khz : 0.0;
+  return HKV_OK;
+}
+
+int hkv_profile_group_stamps(hkv_ctx* ctx, int dev, uint64_t* stamps, size_t n_groups, double* tick_ns) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !stamps || !tick_ns || n_groups > CLK_GROUPS)
+    return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  HKV_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (n_groups)
+    HKV_TRY(hipMemcpy(stamps, d.clk + 16, 2 * n_groups * sizeof(uint64_t), hipMemcpyDeviceToHost), "D2H group stamps");
   *tick_ns = d.wall_khz > 0 ? 1e6 / d.wall_khz : 0.0;
   return HKV_OK;
 }

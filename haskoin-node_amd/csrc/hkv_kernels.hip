@@ -1305,6 +1305,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     if (stamp) clk[4 + slot] = wall_clock64();
   };
   if (threadIdx.x < BF_COUNT) bflag[threadIdx.x] = 0;
+  if (clk != nullptr && threadIdx.x == 0 && blockIdx.x < 4096) clk[16 + 2 * blockIdx.x] = wall_clock64();
   __syncthreads();
   if (wv == 0) mark(STAMP_START);
 
@@ -1466,6 +1467,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     }
     __syncthreads();  // the group's LDS (tables, exchanges, flags' data) is read before the next group's writes
   }
+  if (clk != nullptr && threadIdx.x == 0 && blockIdx.x < 4096) clk[16 + 2 * blockIdx.x + 1] = wall_clock64();
 }
 
 // ---------------------------------------------------------------------------

@@ -104,6 +104,7 @@ EXPORTS = {
                                  POINTER(c_uint64)]),
     "hkv_profile_clock": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double)]),
     "hkv_profile_phases": (c_int, [c_void_p, c_int, POINTER(c_uint64), c_size_t, POINTER(ctypes.c_double)]),
+    "hkv_profile_group_stamps": (c_int, [c_void_p, c_int, POINTER(c_uint64), c_size_t, POINTER(ctypes.c_double)]),
     "hkv_strerror": (c_char_p, [c_int]),
     "hkv_last_hip_error": (c_char_p, []),
     "hkv_device_count": (c_int, []),

@@ -343,6 +343,13 @@ int hkv_profile_clock(hkv_ctx* ctx, int dev, double* sclk_mhz);
  * Synchronises the device. */
 int hkv_profile_phases(hkv_ctx* ctx, int dev, uint64_t* stamps, size_t n, double* tick_ns);
 
+/* Per-workgroup (start, end) constant-rate clock stamps of the last profiled
+ * block-kernel launch (a block: at most 16 signatures per CU): stamps[2g] =
+ * workgroup g's first instruction, stamps[2g + 1] = its last; n_groups <=
+ * 4096. Where the launch's span goes beyond workgroup 0's phase stamps.
+ * Synchronises the device. (Measurement only; no reference counterpart.) */
+int hkv_profile_group_stamps(hkv_ctx* ctx, int dev, uint64_t* stamps, size_t n_groups, double* tick_ns);
+
 const char* hkv_strerror(int err);
 const char* hkv_last_hip_error(void);
 int hkv_device_count(void);
