@@ -283,7 +283,7 @@ def split_phases(v, torch, run, n_groups: int = 0) -> dict:
     out = {name: round((int(stamps[k]) - int(stamps[0])) * tick.value * 1e-3, 1) for k, name in enumerate(PHASES)}
     # every workgroup's (start, end) stamps (the block kernel only): how far
     # the launch's span reaches beyond workgroup 0's phase stamps
-    if n_groups:
+    if n_groups and hasattr(v.lib, "hkv_profile_group_stamps"):
         g = (ctypes.c_uint64 * (2 * n_groups))()
         v.lib.hkv_profile_group_stamps(v.ctx, 0, g, n_groups, ctypes.byref(tick))
         st_, en = [int(g[2 * k]) for k in range(n_groups)], [int(g[2 * k + 1]) for k in range(n_groups)]

@@ -196,16 +196,16 @@ bool split_batch(const DevCtx& d, size_t n) {
   return round_up(n, hkv::WG) <= (size_t)d.grid_max * hkv::WG / HKV_SPLIT_DIV;
 }
 
-// enqueue the verify of n records at d_records; verdict words in out_bits
-// ((n + 31) / 32 words, device memory) or, when null, in d.bits
-// late_join (full-grid batches of standard inputs only): the event after
-// which the records carry their final messages — st waits for it after the
-// ecmult launch, then hkv_late_u1_kernel redoes u1 from them
 // whether a full-grid batch of n runs the 2-wave (mid-size) instance
 bool mid_batch(const DevCtx& d, size_t n) {
   return !split_batch(d, n) && round_up(n, hkv::WG) <= (size_t)d.grid_max * hkv::WG / 2;
 }
 
+// enqueue the verify of n records at d_records; verdict words in out_bits
+// ((n + 31) / 32 words, device memory) or, when null, in d.bits.
+// late_join (full-grid batches of standard inputs only): the event after
+// which the records carry their final messages — st waits for it after the
+// ecmult launch, then the finish kernel redoes u1 from them (LATE).
 // std_pro (mid-size standard-input batches, enqueue_std_chunk): the signature
 // and key come from the batch's txs through the lane prologue — at the head of
 // the ecmult kernel (HKV_STD_FUSED_PROLOGUE) or as a launch before it —
@@ -262,16 +262,15 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   // through y_c = num / den (hkv_kernels.hip §2b). The rare-lane count is
   // re-armed by the verdict kernel; a call that failed between the finish
   // and verdict launches leaves it dirty, so it is zeroed on the stream first.
-  if (late_join != nullptr && !split) {
+  if (late_join != nullptr && !split)
     HKV_TRY(hipStreamWaitEvent(st, late_join, 0), "hipStreamWaitEvent(hash join)");
-    HKV_TRY(hkv::launch_late_u1(d_records, (uint32_t)n, (uint32_t)n_pad, d.im, st), "late u1 launch");
-  }
   if (!split) {
     if (d.rare_dirty) {
       HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), st), "hipMemset(rare counter)");
       d.rare_dirty = false;
     }
-    const hipError_t e2 = hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, st);
+    const hipError_t e2 = hkv::launch_finish(d.im, (uint32_t)n, (uint32_t)n_pad, d.gtab, d.rare_ctr, vbits, n_words, mid,
+                                                 late_join != nullptr ? d_records : nullptr, st);
     if (e2 != hipSuccess) {
       d.rare_dirty = true;
       return hip_fail(e2, "finish launch");
@@ -515,7 +514,7 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   // each record whole; the multisig scan) on the hash stream while st runs
   // the parse half, the prologue and the Q chains, which need only r, s and
   // the key — at mid size all inside the ecmult launch (kernel 1e); st joins
-  // before u1 (hkv_late_u1_kernel) and the finish.
+  // before the finish, which takes u1 from the final records (LATE).
   const bool overlap = !fused && HKV_STD_OVERLAP;
   const bool lane_prologue = overlap && mid_batch(d, n);
   bool forked = false;

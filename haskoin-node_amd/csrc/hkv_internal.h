@@ -97,11 +97,10 @@ struct StdOps {
 hipError_t launch_std_lane_prologue(const StdOps& o, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st);
 hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint32_t n_pad, uint32_t* qs,
                                  uint32_t grid, unsigned long long* clk, hipStream_t st);
-// u1 = m / s and its G digits from the final records (after the overlapped
-// extraction's hash half): a record the hash half zeroed loses FLAG_VALID
-hipError_t launch_late_u1(const void* recs, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st);
+// (mid: the paired-product instance; late_recs: large standard-input batches,
+// u1 and the validity from the final records first)
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
-                         uint32_t* bits, uint32_t n_words, hipStream_t st);
+                         uint32_t* bits, uint32_t n_words, bool mid, const void* late_recs, hipStream_t st);
 hipError_t launch_gen_pool(uint64_t seed, uint32_t npool, uint32_t* pool, hipStream_t st);
 hipError_t launch_gen_records(uint64_t seed, uint64_t index0, uint32_t n, const uint32_t* pool, uint32_t npool,
                               uint32_t unc_permille, uint32_t invalid_permille, void* recs, uint32_t* labels,

@@ -370,21 +370,16 @@ __global__ void __launch_bounds__(WG) hkv_glv_kernel(uint32_t n_pad, uint32_t* _
 }
 
 // 1c'. large standard-input batches (hkv_api.cpp enqueue_std_chunk): the
-//      prologue ran on records whose message the hash half was still writing,
-//      so the G digits are redone here from the final record, after the
-//      join: m = msg mod n, u1 = m s^-1 (IM_C still holds s^-1: the ecmult
-//      kernel writes B' over the Q digits only). A record the hash half
+//      prologue ran before the hash half had written the messages, so the
+//      finish kernel (LATE) first redoes the G digits of its lane from the
+//      final record: m = msg mod n, u1 = m s^-1 (IM_C still holds s^-1: the
+//      ecmult kernel writes B' over the Q digits only). A record the hash half
 //      zeroed (a failed HASH160 / script check) makes the lane invalid.
-__global__ void __launch_bounds__(WG) hkv_late_u1_kernel(const uint32_t* __restrict__ recs, uint32_t n,
-                                                         uint32_t n_pad, uint32_t* __restrict__ im) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
+//      Returns the lane's flags.
+HKV_DEV uint32_t late_u1_lane(const uint32_t* __restrict__ recs, uint32_t i, uint32_t n_pad, uint32_t* __restrict__ im,
+                              uint32_t f) {
   const uint32_t* w = recs + (size_t)i * REC_WORDS;
-  uint32_t f = im[(size_t)IM_FLAGS * n_pad + i];
-  if ((w[24] & 0xFFu) == 0u && (f & FLAG_VALID)) {
-    f &= ~FLAG_VALID;
-    im[(size_t)IM_FLAGS * n_pad + i] = f;
-  }
+  if ((w[24] & 0xFFu) == 0u) f &= ~FLAG_VALID;
   const bool use = (f & FLAG_VALID) != 0;
   sc m, sinv, u1;
 #pragma unroll
@@ -396,6 +391,7 @@ __global__ void __launch_bounds__(WG) hkv_late_u1_kernel(const uint32_t* __restr
 #pragma unroll
   for (int q = 0; q < 4; ++q) { SL[q] = use ? u1.v[q] : 0u; SH[q] = use ? u1.v[4 + q] : 0u; }
   write_gdigits(im, n_pad, i, SL, SH);
+  return f;
 }
 
 // ---------------------------------------------------------------------------
@@ -508,6 +504,7 @@ HKV_DEV void ec_accumulate(gej& acc, bool& inf, const fe& az, const fe& tx, cons
   else gej_accumulate(acc, inf, az, tx, ty, take);
 }
 
+template <bool ILP = false>
 HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab, uint32_t i,
                        bool valid, gej& A, bool& ainf);
 HKV_DEV void gej_add_var(gej& acc, bool& inf, const gej& b, bool binf);
@@ -953,7 +950,7 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
 //     kernel (STDPRO) or, with HKV_STD_FUSED_PROLOGUE=0, as a launch of its
 //     own. Nothing here writes the input's record: the hash half
 //     (hkv_std_input_kernel, on a second stream from the start) writes it
-//     whole, and hkv_late_u1_kernel redoes u1 from it after the join; s^-1
+//     whole, and the finish kernel (LATE) redoes u1 from it after the join; s^-1
 //     stays in IM_C for that.
 HKV_DEV void std_lane_prologue(uint32_t i, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im, const StdArgs& sa) {
   bool glv_ok, n1, n2;
@@ -1550,7 +1547,9 @@ HKV_DEV void gtab_entry(const uint32_t* __restrict__ gtab, int t, uint32_t gd, f
 }
 
 // A = u1 * G of signature i: one affine addition per window, from the
-// per-window tables (no doublings)
+// per-window tables (no doublings); ILP: the paired-product addition (mid-size
+// launches, at most 2 waves per SIMD)
+template <bool ILP>
 HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const uint32_t* __restrict__ gtab, uint32_t i,
                        bool valid, gej& A, bool& ainf) {
   // ---- A = u1 * G: one affine addition per window, table t = 2j + h holds
@@ -1574,7 +1573,7 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
     const bool take = (gd & GD_MAG) != 0;
     fe_cneg(ty, ty, (gd & GD_NEG) != 0);
     const bool was_inf = ainf;
-    gej_accumulate(A, ainf, A.z, tx, ty, take);
+    ec_accumulate<ILP>(A, ainf, A.z, tx, ty, take);
     if (__any(take && was_inf)) gej_accumulate_from_inf(A, ainf, tx, ty, take && was_inf);
     gd = gdn;
     tx = nx;
@@ -1584,13 +1583,23 @@ HKV_DEV void gsum_lane(const uint32_t* __restrict__ im, uint32_t n_pad, const ui
 
 // one signature's finish (hkv_finish_kernel): whole waves call it (the
 // rare-lane compaction ballots)
+// ILP (mid-size launches, at most 2 waves per SIMD): the paired-product
+// forms, independent products interleaved two at a time
+// LATE (large standard-input batches): the lane's G digits and validity come
+// from its final record first (late_u1_lane; its own digit words, read back
+// below by the same lane)
+template <bool ILP, bool LATE>
 HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ gtab,
-                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags) {
+                         uint32_t* __restrict__ rare_ctr, uint32_t i, uint32_t flags,
+                         const uint32_t* __restrict__ recs) {
+  if constexpr (LATE) {
+    if (i < n) flags = late_u1_lane(recs, i, n_pad, im, flags);
+  }
   const bool valid = (i < n) && (flags & FLAG_VALID);
 
   gej A;
   bool ainf;
-  gsum_lane(im, n_pad, gtab, i, valid, A, ainf);
+  gsum_lane<ILP>(im, n_pad, gtab, i, valid, A, ainf);
 
   // ---- B' from the ecmult kernel, w, r (not hoisted above the loop: it
   // would hold 56 more VGPRs through every addition)
@@ -1611,46 +1620,67 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
   // ---- num, num_{r+n}, den (formula above), ordered for short live ranges:
   // a = Y ZA^3, b = YA Z^3 give Y^2 ZA^6 = a^2, YA^2 Z^6 = b^2, den = 2 a b w
   fe ZA2, ZA3, Z2, Z3, U1, H, T, S1, HH, t, num, numn, den;
-  fe_sqr(ZA2, A.z);
-  fe_mul(ZA3, ZA2, A.z);
-  fe_sqr(Z2, B.z);
-  fe_mul(Z3, Z2, B.z);
-  fe_mul(Z2, Z2, w);            // Z^2 w
-  fe_mul(U1, B.x, ZA2);         // X ZA^2
-  fe_mul(t, A.x, Z2);           // XA Z^2 w
-  fe_sub(H, U1, t);
-  const bool hz = fe_is_zero(H);
-  fe_add(S1, t, U1);
-  fe_mul(T, Z2, ZA2);           // Z^2 w ZA^2
-  {
-    fe rf;
+  fe rf, nf;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) rf.v[k] = r[k];
-    fe_mul(t, rf, T);
-    fe_add(S1, S1, t);          // r T + XA Z^2 w + X ZA^2
+  for (int k = 0; k < 8; ++k) {
+    rf.v[k] = r[k];
+    nf.v[k] = SC_N[k];
   }
-  fe_sqr(HH, H);
-  fe a, b;
-  fe_mul(a, B.y, ZA3);
-  fe_mul(b, A.y, Z3);
-  fe_mul(den, a, b);
-  fe_mul(den, den, w);
-  fe_add(den, den, den);        // 2 Y YA Z^3 w ZA^3
-  fe_sqr(num, a);               // Y^2 ZA^6
-  fe_sqr(t, w);
-  fe_mul(t, t, w);              // w^3
-  fe_sqr(b, b);                 // YA^2 Z^6
-  fe_mul(t, t, b);
-  fe_add(num, num, t);
-  fe_mul(t, HH, S1);
-  fe_sub(num, num, t);
-  {
-    fe nf;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) nf.v[k] = SC_N[k];
+  bool hz;
+  if constexpr (ILP) {
+    fe a, b, t2, t3;
+    fe_sqr2(ZA2, A.z, Z2, B.z);
+    fe_mul2(ZA3, ZA2, A.z, Z3, Z2, B.z);
+    fe_mul2(Z2, Z2, w, U1, B.x, ZA2);      // Z^2 w, X ZA^2
+    fe_mul2(t, A.x, Z2, T, Z2, ZA2);       // XA Z^2 w, Z^2 w ZA^2
+    fe_sub(H, U1, t);
+    hz = fe_is_zero(H);
+    fe_add(S1, t, U1);
+    fe_sqrmul(HH, H, t, rf, T);
+    fe_add(S1, S1, t);                     // r T + XA Z^2 w + X ZA^2
+    fe_mul2(a, B.y, ZA3, b, A.y, Z3);
+    fe_sqrmul(num, a, den, a, b);          // Y^2 ZA^6, a b
+    fe_sqrmul(t, w, den, den, w);          // w^2, a b w
+    fe_add(den, den, den);                 // 2 Y YA Z^3 w ZA^3
+    fe_sqrmul(b, b, t, t, w);              // YA^2 Z^6, w^3
+    fe_mul2(t, t, b, t2, HH, S1);
+    fe_add(num, num, t);
+    fe_sub(num, num, t2);
+    fe_mul(t3, T, nf);
+    fe_mul(t3, HH, t3);
+    fe_sub(numn, num, t3);                 // the r + n candidate
+  } else {
+    fe_sqr(ZA2, A.z);
+    fe_mul(ZA3, ZA2, A.z);
+    fe_sqr(Z2, B.z);
+    fe_mul(Z3, Z2, B.z);
+    fe_mul(Z2, Z2, w);            // Z^2 w
+    fe_mul(U1, B.x, ZA2);         // X ZA^2
+    fe_mul(t, A.x, Z2);           // XA Z^2 w
+    fe_sub(H, U1, t);
+    hz = fe_is_zero(H);
+    fe_add(S1, t, U1);
+    fe_mul(T, Z2, ZA2);           // Z^2 w ZA^2
+    fe_mul(t, rf, T);
+    fe_add(S1, S1, t);            // r T + XA Z^2 w + X ZA^2
+    fe_sqr(HH, H);
+    fe a, b;
+    fe_mul(a, B.y, ZA3);
+    fe_mul(b, A.y, Z3);
+    fe_mul(den, a, b);
+    fe_mul(den, den, w);
+    fe_add(den, den, den);        // 2 Y YA Z^3 w ZA^3
+    fe_sqr(num, a);               // Y^2 ZA^6
+    fe_sqr(t, w);
+    fe_mul(t, t, w);              // w^3
+    fe_sqr(b, b);                 // YA^2 Z^6
+    fe_mul(t, t, b);
+    fe_add(num, num, t);
+    fe_mul(t, HH, S1);
+    fe_sub(num, num, t);
     fe_mul(t, T, nf);
     fe_mul(t, HH, t);
-    fe_sub(numn, num, t);       // the r + n candidate
+    fe_sub(numn, num, t);         // the r + n candidate
   }
 
   uint32_t fo = flags;
@@ -1692,12 +1722,15 @@ HKV_DEV void finish_lane(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad, 
   im[(size_t)IM_FLAGS * n_pad + i] = fo;
 }
 
-__global__ void __launch_bounds__(WG, HKV_FINISH_WAVES) hkv_finish_kernel(uint32_t* __restrict__ im, uint32_t n, uint32_t n_pad,
-                                                        const uint32_t* __restrict__ gtab,
-                                                        uint32_t* __restrict__ rare_ctr) {
+template <bool ILP, bool LATE>
+__global__ void __launch_bounds__(WG, ILP ? 2 : HKV_FINISH_WAVES) hkv_finish_kernel(uint32_t* __restrict__ im, uint32_t n,
+                                                                                 uint32_t n_pad,
+                                                                                 const uint32_t* __restrict__ gtab,
+                                                                                 uint32_t* __restrict__ rare_ctr,
+                                                                                 const uint32_t* __restrict__ recs) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n_pad) return;
-  finish_lane(im, n, n_pad, gtab, rare_ctr, i, im[(size_t)IM_FLAGS * n_pad + i]);
+  finish_lane<ILP, LATE>(im, n, n_pad, gtab, rare_ctr, i, im[(size_t)IM_FLAGS * n_pad + i], recs);
 }
 
 // the exact slow path for the finish kernel's rare lanes: y0 = sqrt(w) of
@@ -2393,14 +2426,18 @@ hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint
                      std_args(o));
   return hipGetLastError();
 }
-hipError_t launch_late_u1(const void* recs, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(hkv_late_u1_kernel, dim3(ceil_div(n, WG)), dim3(WG), 0, st, (const uint32_t*)recs, n, n_pad, im);
-  return hipGetLastError();
-}
 hipError_t launch_finish(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_t* gtab, uint32_t* rare_ctr,
-                         uint32_t* bits, uint32_t n_words, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_finish_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n, n_pad, gtab, rare_ctr);
+                         uint32_t* bits, uint32_t n_words, bool mid, const void* late_recs, hipStream_t st) {
+  const uint32_t* lr = static_cast<const uint32_t*>(late_recs);
+  const dim3 g(n_pad / WG), b(WG);
+  if (mid && lr)
+    hipLaunchKernelGGL((hkv_finish_kernel<true, true>), g, b, 0, st, im, n, n_pad, gtab, rare_ctr, lr);
+  else if (mid)
+    hipLaunchKernelGGL((hkv_finish_kernel<true, false>), g, b, 0, st, im, n, n_pad, gtab, rare_ctr, lr);
+  else if (lr)
+    hipLaunchKernelGGL((hkv_finish_kernel<false, true>), g, b, 0, st, im, n, n_pad, gtab, rare_ctr, lr);
+  else
+    hipLaunchKernelGGL((hkv_finish_kernel<false, false>), g, b, 0, st, im, n, n_pad, gtab, rare_ctr, lr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hkv_rare_kernel, dim3(n_pad / WG), dim3(WG), 0, st, im, n_pad, (const uint32_t*)rare_ctr);

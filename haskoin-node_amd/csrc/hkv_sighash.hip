@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
 //     all-zero record when a parse check failed. hkv_std_input_kernel, on a
 //     second stream, then rewrites each record whole (the same r, s and key
 //     bytes plus the sighash, or all zero when a hash check fails), and
-//     hkv_late_u1_kernel takes u1 from the final records.
+//     the finish kernel (LATE) takes u1 from the final records.
 __global__ void __launch_bounds__(WG) hkv_std_parse_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
                                                            const uint32_t* __restrict__ txt,
                                                            const uint8_t* __restrict__ scripts, uint32_t scripts_len,

@@ -111,6 +111,10 @@ EXPORTS = {
     "hkv_version": (c_uint32, []),
 }
 
+# measurement hooks a library variant built before them may lack; every other
+# export is required (tests/test_abi.py checks the in-tree build has them all)
+MEASUREMENT_ONLY = {"hkv_profile_group_stamps"}
+
 _LIB = None
 
 
@@ -125,6 +129,8 @@ def load_library(path: str | None = None):
         raise ImportError(f"libhkv.so not built at {p}; run __graft_entry__.build()")
     lib = ctypes.CDLL(p)
     for name, (res, args) in EXPORTS.items():
+        if name in MEASUREMENT_ONLY and not hasattr(lib, name):
+            continue  # (an older library loaded for a same-box A/B: HKV_LIB)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

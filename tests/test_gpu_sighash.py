@@ -391,8 +391,8 @@ def _device_verify_std(torch, ver, raw_txs, inputs, forkid, records=False):
     return (got, recs.cpu().numpy().tobytes()) if records else got
 
 
-@pytest.mark.parametrize("forkid", [None, 0])
-def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, forkid):
+@pytest.mark.parametrize("n_fill,forkid", [(20000, None), (20000, 0), (2600, None)])
+def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, n_fill, forkid):
     """Above 32,768 inputs the extraction overlaps the ECDSA kernels
     (hkv_api.cpp enqueue_std_chunk): the parse half writes the records the
     prologue and the Q chains read, the hash half rewrites them whole on a
@@ -402,7 +402,8 @@ def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, forkid):
     ANYONECANPAY messages) — spread through a ~37,000-input batch: the final
     records of the generated and mutated inputs are byte-exact against the
     oracle's, every verdict equals the C oracle's on the records the call
-    wrote, and the host entry point agrees."""
+    wrote, and the host entry point agrees. With a 2,600-tx filler (~4,900
+    inputs) the same batch takes the fused pair kernel instead."""
     import hkv
     from hkv import blockgen
     rng = random.Random(4242 + (forkid or 0))
@@ -413,13 +414,13 @@ def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, forkid):
     small_raw = raw + mtx
     small_jobs = jobs + [(t + len(raw), i, p, v) for (t, i, p, v) in mjobs]
     exp_small = [sh.std_input_record(sh.tx_parse(small_raw[t]), i, p, v, forkid) for (t, i, p, v) in small_jobs]
-    btxs, bjobs = blockgen.make_block(ver, torch, n_tx=20000, seed=blockgen.SEED + 99)
+    btxs, bjobs = blockgen.make_block(ver, torch, n_tx=n_fill, seed=blockgen.SEED + 99 + n_fill)
     all_raw = btxs + small_raw
     all_jobs = list(bjobs) + [(t + len(btxs), i, p, v) for (t, i, p, v) in small_jobs]
     order = list(range(len(all_jobs)))
     rng.shuffle(order)
     jobs_sh = [all_jobs[k] for k in order]
-    assert len(jobs_sh) > 32768
+    assert len(jobs_sh) > (32768 if n_fill >= 20000 else 16 * 256)
     got, recs = _device_verify_std(torch, ver, all_raw, jobs_sh, forkid, records=True)
     bad = [pos for pos, k in enumerate(order)
            if k >= len(bjobs) and recs[pos * 168:(pos + 1) * 168] != exp_small[k - len(bjobs)]]

@@ -16,3 +16,6 @@ fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_b32 -o b32 -- \
   python3 tools/block_trace.py --k 5 --batch32 > gpurun_out/${TAG}_b32.log 2>&1 \
   && python3 tools/block_trace.py --report gpurun_out/prof_${TAG}_b32 > gpurun_out/${TAG}_b32_report.txt && echo "trace ok"
+if [ -n "$FULL_BENCH" ]; then
+  timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench_full.log 2>&1 && echo "full bench ok"
+fi

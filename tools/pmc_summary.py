@@ -22,6 +22,8 @@ from collections import defaultdict
 
 def kname(raw: str) -> str:
     """Kernel name without the namespace / argument list. The ecmult instances:
+    round 4 hkv_ecmult_kernel<ILP, STDPRO> (-> "", _mid, _mid_std) and
+    hkv_finish_kernel<ILP, LATE> (-> "", _mid, _late, _mid_late);
     round 3 hkv_ecmult_kernel<ILP> (<false> full grid, <true> -> _mid) and
     hkv_pair_split_kernel<STD> / hkv_block_kernel<STD> (<false> -> _rec,
     <true> -> _std); the round-2
@@ -30,6 +32,13 @@ def kname(raw: str) -> str:
     k = raw.split("(")[0].replace("hkv::", "")
     if k.startswith("void "):
         k = k[5:]
+    # round 4: hkv_ecmult_kernel<ILP, STDPRO> and hkv_finish_kernel<ILP, LATE>
+    if k.startswith("hkv_ecmult_kernel<") or k.startswith("hkv_finish_kernel<"):
+        base, args = k.split("<", 1)
+        flags = [a.strip() == "true" for a in args.rstrip(">").split(",")]
+        if len(flags) == 2:
+            second = "_std" if base == "hkv_ecmult_kernel" else "_late"
+            return base + ("_mid" if flags[0] else "") + (second if flags[1] else "")
     k = k.replace("<false, false>", "").replace("<false, true>", "_mid")
     k = k.replace("<true, true>", "_split").replace("<true, false>", "_split")
     if k.startswith("hkv_pair_split_kernel") or k.startswith("hkv_block_kernel"):
