@@ -10,8 +10,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 # trace pass: the whole default bench (every section); PMC passes: the 1M
 # verify only, so the ecmult counters are those of the timed launch
-FULL="bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-host-path ${BENCH_ARGS}"  # host_path chunks would share the 1M grid
-BENCH="bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-block-mix --no-config0 --no-adversarial --no-headers --no-merkle --no-host-path ${BENCH_ARGS}"
+# (--no-host-path / --no-inproc: their hkv_verify chunks run the same 262,144-lane
+# ecmult grid over more records per launch and would mix into its statistics)
+FULL="bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-host-path --no-inproc ${BENCH_ARGS}"
+BENCH="bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-block-mix --no-config0 --no-adversarial --no-headers --no-merkle --no-host-path --no-inproc ${BENCH_ARGS}"
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o "$name" -- python3 $BENCH \
