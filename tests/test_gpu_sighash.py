@@ -391,7 +391,7 @@ def _device_verify_std(torch, ver, raw_txs, inputs, forkid, records=False):
     return (got, recs.cpu().numpy().tobytes()) if records else got
 
 
-@pytest.mark.parametrize("n_fill,forkid", [(20000, None), (20000, 0), (2600, None)])
+@pytest.mark.parametrize("n_fill,forkid", [(20000, None), (20000, 0), (2600, None), (75000, None)])
 def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, n_fill, forkid):
     """Above 32,768 inputs the extraction overlaps the ECDSA kernels
     (hkv_api.cpp enqueue_std_chunk): the parse half writes the records the
@@ -403,7 +403,10 @@ def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, n_fill, for
     records of the generated and mutated inputs are byte-exact against the
     oracle's, every verdict equals the C oracle's on the records the call
     wrote, and the host entry point agrees. With a 2,600-tx filler (~4,900
-    inputs) the same batch takes the fused pair kernel instead."""
+    inputs) the same batch takes the fused pair kernel instead; with a
+    75,000-tx filler (~138,000 inputs) it runs as two chunks (131,072 inputs
+    through the overlapped form, the rest through the pair kernel) on one
+    stream, sharing the index rows and the fork / join events."""
     import hkv
     from hkv import blockgen
     rng = random.Random(4242 + (forkid or 0))
@@ -420,7 +423,7 @@ def test_std_inputs_full_grid_overlap_vs_oracle(torch, ver, coracle, n_fill, for
     order = list(range(len(all_jobs)))
     rng.shuffle(order)
     jobs_sh = [all_jobs[k] for k in order]
-    assert len(jobs_sh) > (32768 if n_fill >= 20000 else 16 * 256)
+    assert len(jobs_sh) > (131072 if n_fill >= 75000 else 32768 if n_fill >= 20000 else 16 * 256)
     got, recs = _device_verify_std(torch, ver, all_raw, jobs_sh, forkid, records=True)
     bad = [pos for pos, k in enumerate(order)
            if k >= len(bjobs) and recs[pos * 168:(pos + 1) * 168] != exp_small[k - len(bjobs)]]

@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--k", type=int, default=20)
     ap.add_argument("--batch32", action="store_true", help="also the 64,000-tx batch (bench block_mix.batch32)")
     ap.add_argument("--report", default=None, help="summarise a rocprofv3 csv output directory")
+    ap.add_argument("--stamps", action="store_true",
+                    help="one profiled configs[0] call last: print its workgroups' raw start / end clock stamps "
+                         "(s_memrealtime ticks) to set beside the trace's dispatch timestamps")
     a = ap.parse_args()
     if a.report:
         report(a.report)
@@ -65,6 +68,20 @@ def main():
                                         st.cuda_stream)
             torch.cuda.synchronize()
             print(name, what, db.n, flush=True)
+        if a.stamps and name == "configs0":
+            import ctypes
+            v.lib.hkv_profile_enable(v.ctx, 1)
+            v.verify_std_inputs_device(0, db.txs, db.d_jobs.data_ptr(), db.n, -1, db.records.data_ptr(),
+                                       db.bits.data_ptr(), st.cuda_stream)
+            torch.cuda.synchronize()
+            ng = (db.n + 255) // 256 * 256 // 16
+            g = (ctypes.c_uint64 * (2 * ng))()
+            tick = ctypes.c_double()
+            v.lib.hkv_profile_group_stamps(v.ctx, 0, g, ng, ctypes.byref(tick))
+            v.lib.hkv_profile_enable(v.ctx, 0)
+            starts, ends = [g[2 * k] for k in range(ng)], [g[2 * k + 1] for k in range(ng)]
+            print("stamps", {"tick_ns": tick.value, "start_min": min(starts), "start_max": max(starts),
+                             "end_min": min(ends), "end_max": max(ends)}, flush=True)
     v.close()
 
 
