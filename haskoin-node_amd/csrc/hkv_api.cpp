@@ -24,9 +24,6 @@
 #ifndef HKV_STD_OVERLAP
 #define HKV_STD_OVERLAP 1
 #endif
-#ifndef HKV_STD_FUSED_PROLOGUE
-#define HKV_STD_FUSED_PROLOGUE 1
-#endif
 
 namespace {
 
@@ -207,9 +204,8 @@ bool mid_batch(const DevCtx& d, size_t n) {
 // which the records carry their final messages — st waits for it after the
 // ecmult launch, then the finish kernel redoes u1 from them (LATE).
 // std_pro (mid-size standard-input batches, enqueue_std_chunk): the signature
-// and key come from the batch's txs through the lane prologue — at the head of
-// the ecmult kernel (HKV_STD_FUSED_PROLOGUE) or as a launch before it —
-// instead of from records
+// and key come from the batch's txs through the lane prologue at the head of
+// the ecmult kernel instead of from records
 int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hipStream_t st,
                    uint32_t* out_bits = nullptr, hipEvent_t late_join = nullptr,
                    const hkv::StdOps* std_pro = nullptr) {
@@ -239,8 +235,6 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
   if (std_pro != nullptr && !mid) return HKV_E_INTERNAL;  // (the lane prologue is a mid-size form)
   if (!split && std_pro == nullptr)
     HKV_TRY(hkv::launch_prologue(d_records, (uint32_t)n, (uint32_t)n_pad, mode, d.im, st), "prologue launch");
-  if (std_pro != nullptr && !HKV_STD_FUSED_PROLOGUE)
-    HKV_TRY(hkv::launch_std_lane_prologue(*std_pro, (uint32_t)n, (uint32_t)n_pad, d.im, st), "lane prologue launch");
   if (split) {
     rc = ensure_aux(d, n_pad, st);
     if (rc) return rc;
@@ -250,7 +244,7 @@ int enqueue_verify(DevCtx& d, const void* d_records, size_t n, uint32_t mode, hi
                                 : (uint32_t)std::min<size_t>(n_pad / hkv::WG, mid ? d.grid_max / 2 : d.grid_max);
   uint32_t* vbits = out_bits ? out_bits : d.bits;
   const uint32_t n_words = (uint32_t)(out_bits ? (n + 31) / 32 : n_pad / 32);
-  if (std_pro != nullptr && HKV_STD_FUSED_PROLOGUE)
+  if (std_pro != nullptr)
     HKV_TRY(hkv::launch_std_ecmult_mid(*std_pro, d.im, (uint32_t)n, (uint32_t)n_pad, d.qs, blocks,
                                        d.profile ? d.clk : nullptr, st),
             "ecmult launch");
@@ -482,7 +476,7 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
 // kernel (hkv_kernels.hip 2e) does the rest, or nothing when the total is 0.
 int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                      uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
-                     bool lane_prologue, const hkv::MsScan& ms, size_t cap_cand);
+                     const hkv::MsScan& ms, size_t cap_cand);
 int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                       uint32_t* out_bits, hipStream_t st) {
   const bool fused = split_batch(d, n);
@@ -515,8 +509,9 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   // the parse half, the prologue and the Q chains, which need only r, s and
   // the key — at mid size all inside the ecmult launch (kernel 1e); st joins
   // before the finish, which takes u1 from the final records (LATE).
-  const bool overlap = !fused && HKV_STD_OVERLAP;
-  const bool lane_prologue = overlap && mid_batch(d, n);
+  // (mid size: every chunk past the pair kernel's bound on an MI355X, where
+  // the 131,072-input chunk is exactly the 2-wave grid)
+  const bool overlap = !fused && HKV_STD_OVERLAP && mid_batch(d, n);
   bool forked = false;
   if (fused) {
     rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
@@ -524,13 +519,9 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   } else if (overlap) {
     rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
     if (rc) return rc;
-    // (mid-size batches: the parse half runs inside the lane prologue, which
+    // (the parse half runs inside the ecmult launch's lane prologue, which
     // writes no record — the hash half writes each record whole — so the
     // fork comes right after the index rows)
-    if (!lane_prologue)
-      HKV_TRY(hkv::launch_std_parse(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
-                                    forkid, static_cast<uint8_t*>(recs), st),
-              "std parse launch");
     HKV_TRY(hipEventRecord(d.ev_fork, st), "hipEventRecord(fork)");
     HKV_TRY(hipStreamWaitEvent(d.hash_stream, d.ev_fork, 0), "hipStreamWaitEvent(fork)");
     forked = true;
@@ -551,8 +542,7 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
     rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   }
   if (!rc)
-    rc = enqueue_std_rest(d, dt, jobs, n, forkid, recs, out_bits, st, fused, fused_scan, overlap, lane_prologue, ms,
-                          cap_cand);
+    rc = enqueue_std_rest(d, dt, jobs, n, forkid, recs, out_bits, st, fused, fused_scan, overlap, ms, cap_cand);
   // a failed call still orders st after the hash half (the next call's
   // scratch acquire then waits for it too)
   if (rc && forked) (void)hipStreamWaitEvent(st, d.ev_join, 0);
@@ -564,7 +554,7 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
 // multisig scan, the record verify, the multisig tail
 int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                      uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
-                     bool lane_prologue, const hkv::MsScan& ms, size_t cap_cand) {
+                     const hkv::MsScan& ms, size_t cap_cand) {
   uint32_t* desc = ms.desc;
   uint64_t* off = ms.off;
   uint64_t* ctr = ms.counters;
@@ -576,7 +566,7 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
   if (!fused) {
     const hkv::StdOps so{dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, forkid};
     rc = enqueue_verify(d, recs, n, HKV_MODE_HASKOIN, st, out_bits, overlap ? d.ev_join : nullptr,
-                        lane_prologue ? &so : nullptr);
+                        overlap ? &so : nullptr);
     if (rc) return rc;
   }
   uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);

@@ -92,9 +92,8 @@ struct StdOps {
   int32_t forkid;
 };
 // mid-size standard-input batches (the overlapped path): std_parse, prologue,
-// s^-1 and GLV in one lane per input — a launch of its own, or at the head of
-// the mid-size ecmult kernel's lanes (launch_std_ecmult_mid)
-hipError_t launch_std_lane_prologue(const StdOps& o, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st);
+// s^-1 and GLV in one lane per input at the head of the mid-size ecmult
+// kernel's lanes
 hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint32_t n_pad, uint32_t* qs,
                                  uint32_t grid, unsigned long long* clk, hipStream_t st);
 // (mid: the paired-product instance; late_recs: large standard-input batches,
@@ -120,12 +119,8 @@ hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt
 hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                              uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                              uint8_t* recs, hipStream_t st);
-// the overlapped extraction of large batches: the parse half alone (records
-// without the message) and the BIP143 per-tx hashes alone (rows written by
-// launch_tx_index(TX_HASHES_NONE) before)
-hipError_t launch_std_parse(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                            uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid, uint8_t* recs,
-                            hipStream_t st);
+// the overlapped extraction of large batches: the BIP143 per-tx hashes alone
+// (rows written by launch_tx_index(TX_HASHES_NONE) before)
 hipError_t launch_tx_hashes_only(const uint8_t* txs, const uint32_t* tx_off, uint32_t n_tx, uint32_t hashes,
                                  uint32_t* txt, hipStream_t st);
 // multisig inputs: the scan (hkv_sighash.hip section 4; the tail in hkv_kernels.hip)

@@ -946,9 +946,8 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
 //     overlapped path of hkv_api.cpp enqueue_std_chunk): std_parse
 //     (verifyStdInput's parse half), the prologue, s^-1 and the GLV split in
 //     one lane per input (sig_lane_q / sig_lane_g: a per-lane variable-time
-//     safegcd instead of the batch trick) — at the head of the mid-size ecmult
-//     kernel (STDPRO) or, with HKV_STD_FUSED_PROLOGUE=0, as a launch of its
-//     own. Nothing here writes the input's record: the hash half
+//     safegcd instead of the batch trick) at the head of the mid-size ecmult
+//     kernel (STDPRO). Nothing here writes the input's record: the hash half
 //     (hkv_std_input_kernel, on a second stream from the start) writes it
 //     whole, and the finish kernel (LATE) redoes u1 from it after the join; s^-1
 //     stays in IM_C for that.
@@ -973,11 +972,6 @@ HKV_DEV void std_lane_prologue(uint32_t i, uint32_t n, uint32_t n_pad, uint32_t*
     im[(size_t)(IM_W + k) * n_pad + i] = kwv.v[k];
     im[(size_t)(IM_C + k) * n_pad + i] = sinv.v[k];
   }
-}
-__global__ void __launch_bounds__(WG) hkv_std_lane_prologue_kernel(uint32_t n, uint32_t n_pad,
-                                                                   uint32_t* __restrict__ im, StdArgs sa) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i < n_pad) std_lane_prologue(i, n, n_pad, im, sa);
 }
 
 // The signature wave, second half (whole wave: the STD hashes are
@@ -2414,11 +2408,6 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
 }
 static StdArgs std_args(const StdOps& o) {
   return StdArgs{o.txs, o.n_tx, o.txt, o.scripts, o.scripts_len, o.jobs, o.forkid, nullptr, nullptr, nullptr};
-}
-hipError_t launch_std_lane_prologue(const StdOps& o, uint32_t n, uint32_t n_pad, uint32_t* im, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_std_lane_prologue_kernel, dim3(ceil_div(n_pad, WG)), dim3(WG), 0, st, n, n_pad, im,
-                     std_args(o));
-  return hipGetLastError();
 }
 hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint32_t n_pad, uint32_t* qs,
                                  uint32_t grid, unsigned long long* clk, hipStream_t st) {

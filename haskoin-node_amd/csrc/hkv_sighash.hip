@@ -172,26 +172,6 @@ __global__ void __launch_bounds__(WG) hkv_std_input_kernel(const uint8_t* __rest
   std_write_record(r32, x, live, d);
 }
 
-// 3b. the parse half alone (the overlapped extraction of large batches,
-//     hkv_api.cpp enqueue_std_chunk): std_parse, then the record with a zero
-//     message — everything the prologue and the Q chains read — or an
-//     all-zero record when a parse check failed. hkv_std_input_kernel, on a
-//     second stream, then rewrites each record whole (the same r, s and key
-//     bytes plus the sighash, or all zero when a hash check fails), and
-//     the finish kernel (LATE) takes u1 from the final records.
-__global__ void __launch_bounds__(WG) hkv_std_parse_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
-                                                           const uint32_t* __restrict__ txt,
-                                                           const uint8_t* __restrict__ scripts, uint32_t scripts_len,
-                                                           const hkv_input_job* __restrict__ jobs, uint32_t n,
-                                                           int32_t forkid, uint8_t* __restrict__ recs) {
-  const uint32_t jx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (jx >= n) return;
-  StdIn x;
-  std_parse(x, txs, n_tx, txt, scripts, scripts_len, jobs, jx, n, forkid);
-  const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  std_write_record(reinterpret_cast<uint32_t*>(recs + (size_t)jx * REC_SIZE), x, true, zero);
-}
-
 // 4. multisig inputs: the scan (hkv_sighash_dev.h ms_scan_lane), candidate
 //    records, the countMulSig walk
 __global__ void __launch_bounds__(WG) hkv_ms_scan_kernel(const uint8_t* __restrict__ txs, uint32_t n_tx,
@@ -230,14 +210,6 @@ hipError_t launch_tx_hashes_only(const uint8_t* txs, const uint32_t* tx_off, uin
   if (n_tx == 0 || hashes == TX_HASHES_NONE) return hipSuccess;
   hipLaunchKernelGGL(hkv_tx_hash_kernel, dim3((n_tx + xtpb_for(n_tx) - 1) / xtpb_for(n_tx), 3), dim3(xtpb_for(n_tx)), 0,
                      st, txs, tx_off, n_tx, hashes == TX_HASHES_WITNESS ? 1u : 0u, 0u, txt);
-  return hipGetLastError();
-}
-hipError_t launch_std_parse(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
-                            uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid, uint8_t* recs,
-                            hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(hkv_std_parse_kernel, dim3((n + WG - 1) / WG), dim3(WG), 0, st, txs, n_tx, txt, scripts,
-                     scripts_len, jobs, n, forkid, recs);
   return hipGetLastError();
 }
 hipError_t launch_sighash(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
