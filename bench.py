@@ -301,14 +301,16 @@ def split_phases(v, torch, run, n_groups: int = 0) -> dict:
 def block_mix(v, torch, steps: int) -> dict:
     """BASELINE configs[2]: a 2,000-tx P2PKH + P2WPKH block verified end to
     end on device from HBM-resident tx bytes; plus the same pipeline on a
-    32-block batch (64,000 txs) for its throughput. Every generated input is
+    mempool-sized batch (9,000 txs, ~16,000 inputs: the pair kernel's range,
+    4,097-32,768 inputs) and a 32-block batch (64,000 txs: the overlapped
+    full-grid path) for their throughput. Every generated input is
     valid; `rejected` must be 0 (the per-input records are checked against the
     oracle byte for byte in tests/test_gpu_sighash.py, not here)."""
     from hkv import blockgen
     out = {}
     # a dedicated stream: torch's default stream is the null stream (pointer 0)
     bstream = torch.cuda.Stream()
-    for label, n_tx in (("block", 2000), ("batch32", 64000)):
+    for label, n_tx in (("block", 2000), ("pool16k", 9000), ("batch32", 64000)):
         txs, inputs = blockgen.make_block(v, torch, n_tx=n_tx, seed=blockgen.SEED + n_tx)
         db = blockgen.DeviceBlock(torch, txs, inputs)
         out[label], _ = _time_block(v, torch, db, bstream, max(3, steps // (1 if label == "block" else 4)))
