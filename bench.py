@@ -224,14 +224,29 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
     got = np.unpackbits(words.view(np.uint8), bitorder="little")[:db.n].astype(bool)
     res = {"txs": db.n_tx, "inputs": db.n, "tx_bytes": int(db.d_bytes.numel()),
            "accepted": int(got.sum()), "rejected": int(db.n - got.sum())}
+    # k calls back to back between two events, three times after max(k, 10)
+    # untimed calls; the median. Without the warm-up the first loop after a
+    # data set's first call ran slow and each later one faster (configs[0]
+    # 268 / 262 / 255 us, the 64,000-tx batch 1,521 / 1,445 / 1,407 us,
+    # profiles/r04r_bench_reps.log), where 20 calls in, every timing method
+    # agrees (events around 3, 10 or 32 calls, the host clock around 32, one
+    # call alone: 255-258 and 1,378-1,395 us, tools/block_timing.py,
+    # profiles/r04r_block_timing.txt). The reps stay in the line.
     for name, fn in (("total", run), ("extract_sighash", extract)):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(bstream)
-        for _ in range(k):
+        for _ in range(max(k, 10)):
             fn()
-        e1.record(bstream)
-        torch.cuda.synchronize()
-        res[f"{name}_us"] = round(e0.elapsed_time(e1) * 1e3 / k, 1)
+        reps = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(bstream)
+            for _ in range(k):
+                fn()
+            e1.record(bstream)
+            torch.cuda.synchronize()
+            reps.append(e0.elapsed_time(e1) * 1e3 / k)
+        res[f"{name}_us"] = round(sorted(reps)[1], 1)
+        res[f"{name}_us_reps"] = [round(x, 1) for x in reps]
     res["inputs_per_s"] = round(db.n / (res["total_us"] * 1e-6), 1)
     # one block at a time (the stream idle before each call): its latency
     lat = []
@@ -313,7 +328,7 @@ def block_mix(v, torch, steps: int) -> dict:
     for label, n_tx in (("block", 2000), ("pool16k", 9000), ("batch32", 64000)):
         txs, inputs = blockgen.make_block(v, torch, n_tx=n_tx, seed=blockgen.SEED + n_tx)
         db = blockgen.DeviceBlock(torch, txs, inputs)
-        out[label], _ = _time_block(v, torch, db, bstream, max(3, steps // (1 if label == "block" else 4)))
+        out[label], _ = _time_block(v, torch, db, bstream, max(5, steps // (1 if label == "block" else 4)))
     out["workload"] = ("BASELINE configs[2]: 60% P2WPKH (BIP143) / 40% P2PKH (legacy) inputs, 1-3 inputs and 2 "
                        "outputs per tx, SIGHASH_ALL; verifyStdInput semantics, tx bytes resident in HBM")
     return out
