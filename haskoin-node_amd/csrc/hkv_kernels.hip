@@ -879,13 +879,20 @@ HKV_DEV void xch_write(uint32_t* __restrict__ xch, int sigs, uint32_t c, const g
 }
 
 // ---- the roles both small-batch kernels share ----
+// An input's tx bytes and prevout script as the block kernel's LDS copy
+// (TxCache below): t[off] is byte off of the batch's tx buffer, s[k] byte k
+// of the script; null members read HBM.
+struct TxView {
+  const uint8_t* t;
+  const uint8_t* s;
+};
 // the key words of signature i (record words 24..41; STD: parsed from its
 // input, which x receives)
 template <bool STD>
 HKV_DEV void key_words_of(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs, const StdArgs& sa,
-                          uint32_t kw[REC_WORDS], StdIn& x) {
+                          uint32_t kw[REC_WORDS], StdIn& x, TxView v = {nullptr, nullptr}) {
   if constexpr (STD) {
-    std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid);
+    std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid, v.t, v.s);
     std_key_words(kw, x);
   } else {
 #pragma unroll
@@ -895,10 +902,11 @@ HKV_DEV void key_words_of(uint32_t i, uint32_t n, const uint32_t* __restrict__ r
 // Q' = (x w, w^2) on E_w of signature i's key (G, a dummy, for a key that
 // does not parse: the lane's digits are zero)
 template <bool STD>
-HKV_DEV void key_point(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs, const StdArgs& sa, ge& q) {
+HKV_DEV void key_point(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs, const StdArgs& sa, ge& q,
+                       TxView v = {nullptr, nullptr}) {
   uint32_t kw[REC_WORDS];
   StdIn xs = {};
-  key_words_of<STD>(i, n, recs, sa, kw, xs);
+  key_words_of<STD>(i, n, recs, sa, kw, xs, v);
   fe w;
   uint32_t pflags;
   const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
@@ -914,13 +922,23 @@ HKV_DEV void key_point(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs
 template <bool STD>
 HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint32_t mode, uint32_t* __restrict__ im,
                             const uint32_t* __restrict__ recs, const StdArgs& sa, StdIn& x, sc& m, sc& sinv,
-                            bool& use, uint32_t& flags) {
+                            bool& use, uint32_t& flags, TxView v = {nullptr, nullptr},
+                            unsigned long long* sclk = nullptr) {
+#if HKV_SIG_STAMPS == 2
+  auto smark = [&](int slot) {
+    if (sclk != nullptr && (threadIdx.x & 63) == 0) sclk[4 + slot] = wall_clock64();
+  };
+#else
+  auto smark = [&](int) {};
+  (void)sclk;
+#endif
   flags = 0;
   use = false;
   if (!on) return;
   bool ok = i < n, glv_ok, n1, n2;
   uint32_t kw[REC_WORDS];
-  key_words_of<STD>(i, n, recs, sa, kw, x);
+  key_words_of<STD>(i, n, recs, sa, kw, x, v);
+  smark(1);
   sc r, s;
   if constexpr (STD) {
 #pragma unroll
@@ -935,6 +953,7 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
     rec_be256(m.v, w, 0);
   }
   sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
+  smark(8);
   use = ok && glv_ok;
   fe kx, kwv;
   uint32_t pflags = 0;
@@ -984,7 +1003,20 @@ template <bool STD, int SPREAD = 0>
 HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im,
                            const uint32_t* __restrict__ gtab, uint32_t* __restrict__ aux, uint32_t* __restrict__ recs,
                            const StdArgs& sa, uint32_t* shabuf, StdIn& x, sc m, const sc& sinv, bool use,
-                           uint32_t flags) {
+                           uint32_t flags, unsigned long long* sclk = nullptr) {
+  // HKV_SIG_STAMPS (measurement builds only): the signature wave's inner
+  // phases of workgroup 0 overwrite three of the block kernel's phase slots;
+  // 1: lo_table = BIP143 per-tx hashes, digits = sighash, key_sqrt = u1;
+  // 2 (sig_wave_parse): lo_table = the input parse, digits = wave 0's key
+  // point, key_sqrt = s^-1, u2 and the digits
+#if HKV_SIG_STAMPS == 1
+  auto smark = [&](int slot) {
+    if (sclk != nullptr && (threadIdx.x & 63) == 0) sclk[4 + slot] = wall_clock64();
+  };
+#else
+  auto smark = [&](int) {};
+  (void)sclk;
+#endif
   uint32_t stdok = 0;
   if constexpr (STD) {
     uint32_t* r32 = recs + (size_t)(on && i < n ? i : 0) * REC_WORDS;
@@ -994,8 +1026,10 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
     // SINGLE hashOutputs, 8-31 for the tx's BIP143 hashes, which the fused
     // launch computes per input instead of an index-kernel pass)
     if constexpr (SPREAD > 0)  // every input that may sign with the BIP143 form
-      bip143_tx_hashes_spread(sa.txs, x.row, x.ok && (x.segwit || sa.forkid >= 0), r32 + 8, shabuf, SPREAD);
+      bip143_tx_hashes_spread(sa.txs, x.row, x.ok && (x.segwit || sa.forkid >= 0), r32 + 8, shabuf, SPREAD, x.T);
+    smark(1);
     const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8, SPREAD > 0);
+    smark(2);
     if (on) {
       if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
       uint32_t w[8];
@@ -1007,6 +1041,7 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
   }
   if (!on) return;
   sig_lane_g(m, sinv, use, im, n_pad, i);
+  smark(8);
   gej A;
   bool ainf;
   gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
@@ -1021,10 +1056,10 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
 // The key's y0 = sqrt(w) with the key's y parity, and whether w is a square
 template <bool STD>
 HKV_DEV void sqrt_lane(uint32_t i, uint32_t n, uint32_t n_pad, const uint32_t* __restrict__ recs, const StdArgs& sa,
-                       uint32_t* __restrict__ aux) {
+                       uint32_t* __restrict__ aux, TxView v = {nullptr, nullptr}) {
   uint32_t kw[REC_WORDS];
   StdIn xs = {};
-  key_words_of<STD>(i, n, recs, sa, kw, xs);
+  key_words_of<STD>(i, n, recs, sa, kw, xs, v);
   fe x, w, y0, y2, ny;
   uint32_t pflags = 0;
   (void)pubkey_parse_rec_w(kw, x, w, pflags);
@@ -1222,6 +1257,84 @@ constexpr int BLK_K1 = HKV_BLK_K1, BLK_K2 = HKV_BLK_K2;
 static_assert(BLK_K1 >= 2 && BLK_K1 < BLK_K2 && BLK_K2 <= NWIN - 1, "three non-empty segments");
 constexpr int BLK_SIGS = 16;
 constexpr int BLK_TPB = 256;
+
+// The workgroup's 16 input txs and prevout scripts in LDS (STD): every wave's
+// parse of an input (template, pushes, DER, the key) and the signature
+// wave's sighash generator read a tx byte by byte through chains of dependent
+// loads, which a lone wave pays at HBM latency; all 256 threads copy the
+// group's txs (up to TXC_WORDS dwords each, from the dword holding the tx's
+// first byte) and scripts once, behind one barrier. A tx or script that does
+// not fit is read from HBM as before.
+constexpr uint32_t TXC_WORDS = 512;   // 2 KB per input
+constexpr uint32_t SPKC_WORDS = 24;   // 96 B per prevout script
+struct TxCache {
+  uint32_t tx[BLK_SIGS][TXC_WORDS];
+  uint32_t spk[BLK_SIGS][SPKC_WORDS];
+  long long tx_d[BLK_SIGS];   // (first copied dword's address) - txs; -1 << 62: not copied
+  uint32_t spk_b[BLK_SIGS];   // the script's first byte within spk[c]; ~0u: not copied
+};
+template <bool STD> struct TxCacheOf { using type = TxCache; };
+template <> struct TxCacheOf<false> { using type = uint32_t; };
+constexpr long long TXC_NONE = -(1ll << 62);
+
+HKV_DEV void txc_fill(TxCache& tc, const StdArgs& sa, uint32_t base, uint32_t n) {
+  const uint32_t c = threadIdx.x >> 4, k = threadIdx.x & 15u;  // 16 threads per input
+  const uint32_t jx = base + c;
+  uint32_t st = 0, len = 0, so = 0, sl = 0;
+  bool sok = false;
+  if (jx < n) {
+    const hkv_input_job jb = sa.jobs[jx];
+    if (jb.tx < sa.n_tx) {
+      const uint32_t* row = sa.txt + (size_t)jb.tx * TXT_WORDS;
+      if (row[TXT_FLAGS] & TXF_OK) {
+        st = row[TXT_START];
+        len = row[TXT_LOCK] + 4u - st;
+      }
+    }
+    sok = jb.script_off <= sa.scripts_len && sa.scripts_len - jb.script_off >= jb.script_len && jb.script_len != 0;
+    so = jb.script_off;
+    sl = jb.script_len;
+  }
+  // aligned dwords covering the bytes (each holds at least one byte of the
+  // range, so none crosses into a page the range does not touch)
+  const uintptr_t p0 = reinterpret_cast<uintptr_t>(sa.txs) + st, pa = p0 & ~(uintptr_t)3;
+  const uint32_t nw = (uint32_t)((p0 + len - pa + 3) >> 2);
+  const bool tfit = len != 0 && nw <= TXC_WORDS;
+  if (tfit) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pa);
+    for (uint32_t j = k; j < nw; j += 16u) tc.tx[c][j] = src[j];
+  }
+  const uintptr_t q0 = reinterpret_cast<uintptr_t>(sa.scripts) + so, qa = q0 & ~(uintptr_t)3;
+  const uint32_t nws = (uint32_t)((q0 + sl - qa + 3) >> 2);
+  const bool sfit = sok && nws <= SPKC_WORDS;
+  if (sfit) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(qa);
+    for (uint32_t j = k; j < nws; j += 16u) tc.spk[c][j] = src[j];
+  }
+  if (k == 0) {
+    tc.tx_d[c] = tfit ? (long long)(pa - reinterpret_cast<uintptr_t>(sa.txs)) : TXC_NONE;
+    tc.spk_b[c] = sfit ? (uint32_t)(q0 - qa) : ~0u;
+  }
+}
+// input c's view (after the barrier that follows txc_fill)
+HKV_DEV TxView txc_view(const TxCache& tc, uint32_t c) {
+  TxView v;
+  const long long d = tc.tx_d[c];
+  const uint32_t b = tc.spk_b[c];
+  // v.t lies outside the LDS object (only v.t + off, off in the tx, lands in
+  // it), so it is formed on the 64-bit flat address as an integer: pointer
+  // arithmetic would let the compiler move the subtraction into the 32-bit
+  // LDS address space, where it wraps
+  const uintptr_t g = reinterpret_cast<uintptr_t>(static_cast<const void*>(&tc.tx[c][0]));
+  v.t = d != TXC_NONE ? reinterpret_cast<const uint8_t*>(g - (uintptr_t)d) : nullptr;
+  v.s = b != ~0u ? reinterpret_cast<const uint8_t*>(&tc.spk[c][0]) + b : nullptr;
+  return v;
+}
+template <bool STD, class C>
+HKV_DEV TxView blk_view(const C& tc, uint32_t c) {
+  if constexpr (STD) return txc_view(tc, c);
+  else return TxView{nullptr, nullptr};
+}
 enum : int { BF_SIG = 0, BF_A = 1, BF_Y = 2, BF_T = 3, BF_Q = 4, BF_U = 5, BF_COUNT = 6 };
 constexpr int STAMP_CHAIN_MID = STAMP_COUNT;  // the twelfth phase slot (hkv_profile_phases reads 12)
 // publish: every prior write of the wave (LDS and global) before the flag
@@ -1288,11 +1401,15 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   __shared__ uint32_t qpub[3][8][BLK_SIGS];     // Q1 = (X, Y, Z), wave 1 -> wave 3
   __shared__ uint32_t shabuf[STD ? 16 * WG : 1];
   __shared__ uint32_t bflag[BF_COUNT];
+  __shared__ typename TxCacheOf<STD>::type tcache;  // STD: the group's txs and scripts
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
+#if HKV_SIG_STAMPS
+    if (slot == STAMP_TABLE0 || slot == STAMP_P || slot == STAMP_SQRT) return;  // the signature wave's
+#endif
     if (stamp) clk[4 + slot] = wall_clock64();
   };
   if (threadIdx.x < BF_COUNT) bflag[threadIdx.x] = 0;
@@ -1303,6 +1420,10 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   uint32_t seq = 0;
   for (uint32_t base = blockIdx.x * BLK_SIGS; base < n_pad; base += gridDim.x * BLK_SIGS) {
     ++seq;
+    if constexpr (STD) {
+      txc_fill(tcache, sa, base, n);
+      __syncthreads();
+    }
     if (wv == 2) {
       const uint32_t i = base + ln;
       const bool on = ln < BLK_SIGS;
@@ -1310,10 +1431,12 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       bool use;
       sc sinv, m;
       StdIn x = {};
-      sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags);
+      sig_wave_parse<STD>(i, on, n, n_pad, mode, im, recs, sa, x, m, sinv, use, flags,
+                          blk_view<STD>(tcache, ln & (BLK_SIGS - 1)), stamp ? clk : nullptr);
       blk_post(&bflag[BF_SIG], seq);
       mark(STAMP_SIG);
-      sig_wave_gsum<STD, BLK_SIGS>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags);
+      sig_wave_gsum<STD, BLK_SIGS>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags,
+                                    stamp ? clk : nullptr);
       blk_post(&bflag[BF_A], seq);
       mark(STAMP_GSUM);
       // STD: the multisig scan of the group's inputs (off every critical path)
@@ -1333,7 +1456,10 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     fe Zg, zb, P, Z;                              // table scale, base point's Z
     if (wv == 0) {
       ge q;
-      key_point<STD>(i, n, recs, sa, q);
+      key_point<STD>(i, n, recs, sa, q, blk_view<STD>(tcache, c));
+#if HKV_SIG_STAMPS == 2
+      if (stamp) clk[4 + STAMP_P] = wall_clock64();
+#endif
       fe_sel(P, q.x, q.y, odd);
       fe_set_u32(zb, 1);
       pair_table(P, half, odd, qlds[0], hlds[0], ln, Zg);
@@ -1343,7 +1469,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       const uint32_t cq = ln >> 2, qd = ln & 3u;
       const uint32_t m0 = qd == 0 ? ~0u : 0u, m1 = qd == 1 ? ~0u : 0u, m2 = qd == 2 ? ~0u : 0u;
       ge q;
-      key_point<STD>(base + cq, n, recs, sa, q);
+      key_point<STD>(base + cq, n, recs, sa, q, blk_view<STD>(tcache, cq));
       fe V;
       fe_set_u32(V, 1);
       fe_sel(V, V, q.y, m1);
@@ -1368,7 +1494,7 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       pair_table(P, half, odd, qlds[1], hlds[1], ln, Zg);
       mark(STAMP_TABLE1);
     } else {
-      if (ln < BLK_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux);
+      if (ln < BLK_SIGS) sqrt_lane<STD>(base + ln, n, n_pad, recs, sa, aux, blk_view<STD>(tcache, ln));
       blk_post(&bflag[BF_Y], seq);
       mark(STAMP_SQRT);
       blk_wait(&bflag[BF_Q], seq);  // Q1 from wave 1

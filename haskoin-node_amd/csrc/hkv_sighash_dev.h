@@ -770,13 +770,19 @@ struct StdIn {
   const uint8_t* wprog;
   bool has_kh, has_rd, has_ws;
   uint32_t r[8], s[8];        // the decoded signature (limbs)
+  const uint8_t* T;           // the tx bytes the pointers above index (txs, or the input's LDS copy)
 };
 
 // Part A: template match, strict DER decode (low S, hashtype), pubkey bytes.
 // No hashing: everything the ECDSA chains need (r, s, the key) is known here.
 HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx, const uint32_t* __restrict__ txt,
                        const uint8_t* __restrict__ scripts, uint32_t scripts_len,
-                       const hkv_input_job* __restrict__ jobs, uint32_t jx, uint32_t n, int32_t forkid) {
+                       const hkv_input_job* __restrict__ jobs, uint32_t jx, uint32_t n, int32_t forkid,
+                       const uint8_t* tview = nullptr, const uint8_t* sview = nullptr) {
+  // tview / sview: the input's tx and prevout script copied to LDS (the block
+  // kernel's TxCache): tview[off] is byte off of txs, sview[k] byte k of the
+  // script; null: read from HBM
+  const uint8_t* T = tview != nullptr ? tview : txs;
   const bool in_range = jx < n;
   bool ok = false;
   const uint32_t* row = txt;
@@ -807,24 +813,24 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
       ok = (row[TXT_FLAGS] & TXF_OK) && jb.input < row[TXT_NIN];
     }
     if (ok) {
-      spk = scripts + jb.script_off;
+      spk = sview != nullptr ? sview : scripts + jb.script_off;
       const uint32_t L = jb.script_len;
       uint32_t in_off, ss_off, ss_len, seq_off;
-      walk_input(txs, row[TXT_INS], jb.input, in_off, ss_off, ss_len, seq_off);
+      walk_input(T, row[TXT_INS], jb.input, in_off, ss_off, ss_len, seq_off);
       const uint32_t ss_end = ss_off + ss_len;
       uint32_t c = ss_off, pub_off = 0;
       // witness program to open: 1 P2WPKH [sig, pub], 2 P2WSH [stack.., ws]
       uint32_t open_wit = 0;
       if (is_p2pk(spk, L)) {  // scriptSig = <sig>; pubkey from the prevout
-        ok = read_push(txs, c, ss_end, sig_off, sig_len) && c == ss_end;
+        ok = read_push(T, c, ss_end, sig_off, sig_len) && c == ss_end;
         pub = spk + 1;
         pub_len = L - 2;
         code = spk;
         code_len = L;
       } else if (is_p2pkh(spk, L)) {  // scriptSig = <sig> <pubkey>
-        ok = read_push(txs, c, ss_end, sig_off, sig_len) && read_push(txs, c, ss_end, pub_off, pub_len) &&
+        ok = read_push(T, c, ss_end, sig_off, sig_len) && read_push(T, c, ss_end, pub_off, pub_len) &&
              c == ss_end;
-        pub = txs + pub_off;
+        pub = T + pub_off;
         kh = spk + 3;
         has_kh = true;
         code = spk;
@@ -843,7 +849,7 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
         uint32_t np = 0, o0 = 0, l0 = 0, o1 = 0, l1 = 0, ol = 0, ll = 0;
         while (ok && c < ss_end) {
           uint32_t d_off = 0, d_len = 0;
-          ok = read_push(txs, c, ss_end, d_off, d_len);
+          ok = read_push(T, c, ss_end, d_off, d_len);
           if (np == 0) { o0 = d_off; l0 = d_len; }
           if (np == 1) { o1 = d_off; l1 = d_len; }
           ol = d_off;
@@ -851,7 +857,7 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
           ++np;
         }
         ok = ok && np >= 1;
-        rd = txs + ol;
+        rd = T + ol;
         rd_len = ll;
         has_rd = true;
         if (ok) {
@@ -874,7 +880,7 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
           } else if (is_p2pkh(rd, ll)) {  // P2SH-P2PKH: <sig> <pubkey> <redeem>
             ok = np == 3;
             sig_off = o0; sig_len = l0;
-            pub = txs + o1;
+            pub = T + o1;
             pub_len = l1;
             kh = rd + 3;
             has_kh = true;
@@ -889,38 +895,38 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
       }
       if (ok && open_wit) {
         ok = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
-        uint32_t w = ok ? walk_witness(txs, row[TXT_OUTS_END], jb.input) : 0u;
-        const uint32_t cnt = ok ? get_varint(txs, w) : 0u;
+        uint32_t w = ok ? walk_witness(T, row[TXT_OUTS_END], jb.input) : 0u;
+        const uint32_t cnt = ok ? get_varint(T, w) : 0u;
         if (open_wit == 1) {  // [sig, pubkey]
           ok = ok && cnt == 2u;
           if (ok) {
-            sig_len = get_varint(txs, w);
+            sig_len = get_varint(T, w);
             sig_off = w;
             w += sig_len;
-            pub_len = get_varint(txs, w);
-            pub = txs + w;
+            pub_len = get_varint(T, w);
+            pub = T + w;
           }
           segwit = p2wpkh = true;
         } else {  // [sig, ws] (P2PK) or [sig, pubkey, ws] (P2PKH)
           ok = ok && (cnt == 2u || cnt == 3u);
           if (ok) {
-            sig_len = get_varint(txs, w);
+            sig_len = get_varint(T, w);
             sig_off = w;
             w += sig_len;
             uint32_t l1 = 0, o1 = 0;
             if (cnt == 3u) {
-              l1 = get_varint(txs, w);
+              l1 = get_varint(T, w);
               o1 = w;
               w += l1;
             }
-            ws_len = get_varint(txs, w);
-            ws = txs + w;
+            ws_len = get_varint(T, w);
+            ws = T + w;
             has_ws = true;
             if (cnt == 2u && is_p2pk(ws, ws_len)) {
               pub = ws + 1;
               pub_len = ws_len - 2;
             } else if (cnt == 3u && is_p2pkh(ws, ws_len)) {
-              pub = txs + o1;
+              pub = T + o1;
               pub_len = l1;
               kh = ws + 3;
               has_kh = true;
@@ -934,13 +940,13 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
         }
       }
     }
-    if (ok) ok = decode_tx_sig(txs, sig_off, sig_len, forkid, r, s, sh);
+    if (ok) ok = decode_tx_sig(T, sig_off, sig_len, forkid, r, s, sh);
     if (ok) ok = pubkey_bytes_ok(pub, pub_len);
   }
   x.ok = ok; x.row = row; x.spk = spk; x.input = input; x.sh = sh; x.value = value;
   x.pub = pub; x.pub_len = pub_len; x.code = code; x.code_len = code_len; x.segwit = segwit; x.p2wpkh = p2wpkh;
   x.kh = kh; x.rd = rd; x.rd_len = rd_len; x.ws = ws; x.ws_len = ws_len; x.wprog = wprog;
-  x.has_kh = has_kh; x.has_rd = has_rd; x.has_ws = has_ws;
+  x.has_kh = has_kh; x.has_rd = has_rd; x.has_ws = has_ws; x.T = T;
 #pragma unroll
   for (int k = 0; k < 8; ++k) { x.r[k] = r[k]; x.s[k] = s[k]; }
 }
@@ -977,9 +983,13 @@ HKV_DEV void bip143_tx_hashes(const uint8_t* __restrict__ txs, const uint32_t* r
 // block-synchronous stream; the digests go to input c's h3 scratch. Call
 // from wave-uniform control flow with every lane of the wave.
 HKV_DEV void bip143_tx_hashes_spread(const uint8_t* __restrict__ txs, const uint32_t* row, bool need, uint32_t* h3,
-                                     uint32_t* buf, uint32_t G) {
+                                     uint32_t* buf, uint32_t G, const uint8_t* tview = nullptr) {
   const uint32_t L = threadIdx.x & 63u, c = L % G, which = L / G;
   const uint64_t rp = reinterpret_cast<uint64_t>(row), hp = reinterpret_cast<uint64_t>(h3);
+  // input c's tx bytes (its LDS copy when the caller has one)
+  const uint64_t tp = reinterpret_cast<uint64_t>(tview != nullptr ? tview : txs);
+  const uint64_t tc = (uint64_t)(uint32_t)__shfl((int)(uint32_t)tp, (int)c) |
+                      ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(tp >> 32), (int)c) << 32);
   const uint64_t rc = (uint64_t)(uint32_t)__shfl((int)(uint32_t)rp, (int)c) |
                       ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rp >> 32), (int)c) << 32);
   const uint64_t hc = (uint64_t)(uint32_t)__shfl((int)(uint32_t)hp, (int)c) |
@@ -989,7 +999,7 @@ HKV_DEV void bip143_tx_hashes_spread(const uint8_t* __restrict__ txs, const uint
   Gen g;
   uint32_t h[8], d[8];
   gen_clear(g);
-  g.T = txs;
+  g.T = reinterpret_cast<const uint8_t*>(tc);
   if (go) {
     if (which == 2) {  // hashOutputs (each output re-serialised canonically)
       g.ooff = rw[TXT_OUTS_FIRST]; g.ocnt = rw[TXT_NOUT]; g.ret = PH_DONE; g.phase = PH_O_VAL;
@@ -1028,6 +1038,7 @@ HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid,
   const uint8_t *kh = x.kh, *rd = x.rd, *ws = x.ws, *wprog = x.wprog;
   const uint32_t rd_len = x.rd_len, ws_len = x.ws_len;
   const uint64_t value = x.value;
+  const uint8_t* T = x.T != nullptr ? x.T : txs;
   uint32_t* r32 = single_ho;
   Gen g;
   uint32_t h[8];
@@ -1064,11 +1075,11 @@ HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid,
   // witness script (P2WSH)
   JobCtx c;
   c.forkid_form = false; c.one = false; c.single_hash = false;
-  if (ok) job_setup(c, txs, row, input, sh, segwit, forkid);
+  if (ok) job_setup(c, T, row, input, sh, segwit, forkid);
   const bool need_single = ok && c.single_hash;
   if (__any(need_single)) {
     gen_clear(g);
-    g.T = txs; g.ooff = c.single_off; g.ocnt = 1; g.ret = PH_DONE; g.phase = PH_O_VAL;
+    g.T = T; g.ooff = c.single_off; g.ocnt = 1; g.ret = PH_DONE; g.phase = PH_O_VAL;
     sha256_stream(h, g, need_single, buf);
     sha256d_finish(d, h);
     if (need_single) {
@@ -1079,10 +1090,10 @@ HKV_DEV bool std_hash(StdIn& x, const uint8_t* __restrict__ txs, int32_t forkid,
   const bool live = ok && !c.one;
   if (h3 != nullptr && !h3_ready) {
     const bool need_tx = live && c.forkid_form;
-    if (__any(need_tx)) bip143_tx_hashes(txs, row, need_tx, h3, buf);
+    if (__any(need_tx)) bip143_tx_hashes(T, row, need_tx, h3, buf);
   }
   if (!live) gen_clear(g);
-  else gen_job(g, c, txs, row, code, p2wpkh ? 20u : code_len, p2wpkh, value, r32, h3);
+  else gen_job(g, c, T, row, code, p2wpkh ? 20u : code_len, p2wpkh, value, r32, h3);
   sha256_stream(h, g, live, buf);
   sha256d_finish(d, h);
   x.ok = ok;
