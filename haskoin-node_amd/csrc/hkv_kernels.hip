@@ -890,9 +890,9 @@ struct TxView {
 // input, which x receives)
 template <bool STD>
 HKV_DEV void key_words_of(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs, const StdArgs& sa,
-                          uint32_t kw[REC_WORDS], StdIn& x, TxView v = {nullptr, nullptr}) {
+                          uint32_t kw[REC_WORDS], StdIn& x, TxView v = {nullptr, nullptr}, bool key_only = false) {
   if constexpr (STD) {
-    std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid, v.t, v.s);
+    std_parse(x, sa.txs, sa.n_tx, sa.txt, sa.scripts, sa.scripts_len, sa.jobs, i, n, sa.forkid, v.t, v.s, key_only);
     std_key_words(kw, x);
   } else {
 #pragma unroll
@@ -906,7 +906,7 @@ HKV_DEV void key_point(uint32_t i, uint32_t n, const uint32_t* __restrict__ recs
                        TxView v = {nullptr, nullptr}) {
   uint32_t kw[REC_WORDS];
   StdIn xs = {};
-  key_words_of<STD>(i, n, recs, sa, kw, xs, v);
+  key_words_of<STD>(i, n, recs, sa, kw, xs, v, true);
   fe w;
   uint32_t pflags;
   const bool pk = pubkey_parse_rec_w(kw, q.x, w, pflags) && i < n;
@@ -1059,7 +1059,7 @@ HKV_DEV void sqrt_lane(uint32_t i, uint32_t n, uint32_t n_pad, const uint32_t* _
                        uint32_t* __restrict__ aux, TxView v = {nullptr, nullptr}) {
   uint32_t kw[REC_WORDS];
   StdIn xs = {};
-  key_words_of<STD>(i, n, recs, sa, kw, xs, v);
+  key_words_of<STD>(i, n, recs, sa, kw, xs, v, true);
   fe x, w, y0, y2, ny;
   uint32_t pflags = 0;
   (void)pubkey_parse_rec_w(kw, x, w, pflags);

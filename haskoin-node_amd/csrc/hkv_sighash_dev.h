@@ -778,10 +778,13 @@ struct StdIn {
 HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx, const uint32_t* __restrict__ txt,
                        const uint8_t* __restrict__ scripts, uint32_t scripts_len,
                        const hkv_input_job* __restrict__ jobs, uint32_t jx, uint32_t n, int32_t forkid,
-                       const uint8_t* tview = nullptr, const uint8_t* sview = nullptr) {
+                       const uint8_t* tview = nullptr, const uint8_t* sview = nullptr, bool key_only = false) {
   // tview / sview: the input's tx and prevout script copied to LDS (the block
   // kernel's TxCache): tview[off] is byte off of txs, sview[k] byte k of the
-  // script; null: read from HBM
+  // script; null: read from HBM. key_only: the caller needs the key and the
+  // template checks, not the signature (the chain waves of the small-batch
+  // kernels: the verdict takes its validity from the signature wave's full
+  // parse), so the DER decode is skipped and r, s stay zero
   const uint8_t* T = tview != nullptr ? tview : txs;
   const bool in_range = jx < n;
   bool ok = false;
@@ -940,7 +943,7 @@ HKV_DEV void std_parse(StdIn& x, const uint8_t* __restrict__ txs, uint32_t n_tx,
         }
       }
     }
-    if (ok) ok = decode_tx_sig(T, sig_off, sig_len, forkid, r, s, sh);
+    if (ok && !key_only) ok = decode_tx_sig(T, sig_off, sig_len, forkid, r, s, sh);
     if (ok) ok = pubkey_bytes_ok(pub, pub_len);
   }
   x.ok = ok; x.row = row; x.spk = spk; x.input = input; x.sh = sh; x.value = value;
