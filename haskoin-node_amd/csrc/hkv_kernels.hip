@@ -997,8 +997,9 @@ HKV_DEV void std_lane_prologue(uint32_t i, uint32_t n, uint32_t n_pad, uint32_t*
 // block-synchronous): STD — the script checks, the sighash and the input's
 // verify record; then u1 = m / s and A = u1 G into aux.
 // SPREAD: the signature inputs are lanes 0..SPREAD-1 and the wave's other
-// lanes compute the three BIP143 per-tx hashes side by side (the block
-// kernel, SPREAD = 16); 0: each input's lane computes them in turn.
+// lanes compute the three BIP143 per-tx hashes side by side (SPREAD = 16);
+// 0: each input's lane computes them in turn; -1: another wave has put them
+// in r32 + 8 (the block kernel's wave 0, blk_tx_hashes).
 template <bool STD, int SPREAD = 0>
 HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint32_t* __restrict__ im,
                            const uint32_t* __restrict__ gtab, uint32_t* __restrict__ aux, uint32_t* __restrict__ recs,
@@ -1028,7 +1029,7 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
     if constexpr (SPREAD > 0)  // every input that may sign with the BIP143 form
       bip143_tx_hashes_spread(sa.txs, x.row, x.ok && (x.segwit || sa.forkid >= 0), r32 + 8, shabuf, SPREAD, x.T);
     smark(1);
-    const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8, SPREAD > 0);
+    const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8, SPREAD != 0);
     smark(2);
     if (on) {
       if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
@@ -1247,11 +1248,13 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
 //     workgroup scope) instead of workgroup barriers, so no wave waits at a
 //     barrier for a phase it does not need.
 // ---------------------------------------------------------------------------
+// (17, 27) since the chain waves parse keys without the DER signature (wave
+// 1's doublings start 6 us earlier; profiles/r04r_blk_k/summary.txt): was (18, 28)
 #ifndef HKV_BLK_K1
-#define HKV_BLK_K1 18
+#define HKV_BLK_K1 17
 #endif
 #ifndef HKV_BLK_K2
-#define HKV_BLK_K2 28
+#define HKV_BLK_K2 27
 #endif
 constexpr int BLK_K1 = HKV_BLK_K1, BLK_K2 = HKV_BLK_K2;
 static_assert(BLK_K1 >= 2 && BLK_K1 < BLK_K2 && BLK_K2 <= NWIN - 1, "three non-empty segments");
@@ -1335,7 +1338,29 @@ HKV_DEV TxView blk_view(const C& tc, uint32_t c) {
   if constexpr (STD) return txc_view(tc, c);
   else return TxView{nullptr, nullptr};
 }
-enum : int { BF_SIG = 0, BF_A = 1, BF_Y = 2, BF_T = 3, BF_Q = 4, BF_U = 5, BF_COUNT = 6 };
+// The three BIP143 per-tx hashes of the group's inputs on one wave (lane
+// w 16 + c: hash w of input c's tx, bip143_tx_hashes_spread) into each
+// input's record scratch (words 8..31, read by its sighash and overwritten
+// by its record). Every input whose tx carries a witness section, or every
+// input on a fork-id network, gets them; the sighash uses them only for the
+// BIP143 form, which needs a witness tx (or FORKID).
+HKV_DEV void blk_tx_hashes(const StdArgs& sa, const TxCache& tc, uint32_t base, uint32_t n, uint32_t* recs,
+                           uint32_t* shabuf) {
+  const uint32_t c = (threadIdx.x & 63u) & (BLK_SIGS - 1), i = base + c;
+  const uint32_t* row = sa.txt;
+  bool need = false;
+  if (i < n) {
+    const hkv_input_job jb = sa.jobs[i];
+    if (jb.tx < sa.n_tx) {
+      row = sa.txt + (size_t)jb.tx * TXT_WORDS;
+      const uint32_t f = row[TXT_FLAGS];
+      need = (f & TXF_OK) && ((f & TXF_WITNESS) || sa.forkid >= 0);
+    }
+  }
+  bip143_tx_hashes_spread(sa.txs, row, need, recs + (size_t)(i < n ? i : 0u) * REC_WORDS + 8, shabuf, BLK_SIGS,
+                          txc_view(tc, c).t);
+}
+enum : int { BF_SIG = 0, BF_A = 1, BF_Y = 2, BF_T = 3, BF_Q = 4, BF_U = 5, BF_H = 6, BF_COUNT = 7 };
 constexpr int STAMP_CHAIN_MID = STAMP_COUNT;  // the twelfth phase slot (hkv_profile_phases reads 12)
 // publish: every prior write of the wave (LDS and global) before the flag
 HKV_DEV void blk_post(uint32_t* f, uint32_t seq) {
@@ -1435,8 +1460,9 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
                           blk_view<STD>(tcache, ln & (BLK_SIGS - 1)), stamp ? clk : nullptr);
       blk_post(&bflag[BF_SIG], seq);
       mark(STAMP_SIG);
-      sig_wave_gsum<STD, BLK_SIGS>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use, flags,
-                                    stamp ? clk : nullptr);
+      if constexpr (STD) blk_wait(&bflag[BF_H], seq);  // the BIP143 per-tx hashes (wave 0)
+      sig_wave_gsum<STD, (STD ? -1 : BLK_SIGS)>(i, on, n, n_pad, im, gtab, aux, recs, sa, shabuf, x, m, sinv, use,
+                                                flags, stamp ? clk : nullptr);
       blk_post(&bflag[BF_A], seq);
       mark(STAMP_GSUM);
       // STD: the multisig scan of the group's inputs (off every critical path)
@@ -1464,6 +1490,12 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       fe_set_u32(zb, 1);
       pair_table(P, half, odd, qlds[0], hlds[0], ln, Zg);
       mark(STAMP_TABLE0);
+      // STD: the BIP143 per-tx hashes for the signature wave, in the time
+      // this wave waits for the digits (the s^-1 the signature wave computes)
+      if constexpr (STD) {
+        blk_tx_hashes(sa, tcache, base, n, recs, shabuf);
+        blk_post(&bflag[BF_H], seq);
+      }
     } else if (wv == 1) {
       // Q1, Q2 on four lanes per signature (lanes 4c'..4c'+3: X | Y | Z | .)
       const uint32_t cq = ln >> 2, qd = ln & 3u;
