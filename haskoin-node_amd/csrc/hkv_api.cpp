@@ -21,6 +21,9 @@
 #include "hkv_layout.h"
 #include "hkv_plan.h"
 
+#ifndef HKV_BLOCK_ROWS  // the block kernel builds its inputs' tx index rows (0: an index launch first)
+#define HKV_BLOCK_ROWS 1
+#endif
 #ifndef HKV_STD_OVERLAP
 #define HKV_STD_OVERLAP 1
 #endif
@@ -442,7 +445,8 @@ int enqueue_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, 
 // <true>): the chains start from the parsed keys and signatures while the
 // signature wave computes the sighashes and script checks beside them.
 int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
-                             void* recs, uint32_t* out_bits, const hkv::MsScan* ms, hipStream_t st) {
+                             void* recs, uint32_t* out_bits, const hkv::MsScan* ms, const uint32_t* tx_off,
+                             hipStream_t st) {
   const size_t n_pad = round_up(n, hkv::WG);
   int rc = ensure_dev_buffers(d, n_pad);
   if (!rc) rc = ensure_aux(d, n_pad, st);
@@ -456,7 +460,7 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
   HKV_TRY(hkv::launch_std_verify_split(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n,
                                        (uint32_t)n_pad, forkid, static_cast<uint8_t*>(recs), d.im, d.gtab, d.qs,
                                        d.aux, out_bits, (uint32_t)((n + 31) / 32), d.profile ? d.clk : nullptr,
-                                       (uint32_t)d.n_cu, ms, st),
+                                       (uint32_t)d.n_cu, ms, tx_off, st),
           "std-input verify launch");
   if (d.profile) {
     HKV_TRY(hipEventRecord(e[2], st), "hipEventRecord");
@@ -514,8 +518,16 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   const bool overlap = !fused && HKV_STD_OVERLAP && mid_batch(d, n);
   bool forked = false;
   if (fused) {
-    rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
-    if (!rc) rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, fused_scan ? &ms : nullptr, st);
+    // the block kernel (fused_scan) builds the rows of its inputs' txs itself
+    // (kernel 2d txc_fill): no index launch before it
+    const bool rows = fused_scan && HKV_BLOCK_ROWS;
+    if (rows)
+      rc = grow(reinterpret_cast<void**>(&d.txt), &d.txt_cap, (size_t)dt->n_tx * hkv::TXT_WORDS * 4, "hipMalloc(txt)");
+    else
+      rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
+    if (!rc)
+      rc = enqueue_std_verify_split(d, dt, jobs, n, forkid, recs, out_bits, fused_scan ? &ms : nullptr,
+                                    rows ? dt->offsets : nullptr, st);
   } else if (overlap) {
     rc = enqueue_tx_index(d, dt, st, hkv::TX_HASHES_NONE);
     if (rc) return rc;

@@ -73,12 +73,14 @@ struct MsTail {
 hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st);
 uint32_t ms_tail_slots(uint32_t n_cu);  // signatures in flight (im / aux slots the tail needs)
 // small batches of standard inputs in one launch; with ms, the block kernel
-// (std_split_scans) also runs the multisig scan
+// (std_split_scans) also runs the multisig scan; with tx_off (the block
+// kernel only), it builds the index rows of its inputs' txs into txt itself
+// (no index launch before it)
 hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
-                                   uint32_t n_cu, const MsScan* ms, hipStream_t st);
+                                   uint32_t n_cu, const MsScan* ms, const uint32_t* tx_off, hipStream_t st);
 bool std_split_scans(uint32_t n_pad, uint32_t n_cu);
 // y-free full-grid batches: u1 * G, the y0 = num / den reduction and the verdict bitmap
 // the operands of a standard-input batch (txs, index rows, prevout scripts, jobs)

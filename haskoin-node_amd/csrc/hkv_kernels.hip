@@ -466,6 +466,9 @@ struct StdArgs {
   uint32_t* ms_desc;
   uint64_t* ms_off;
   unsigned long long* ms_ctr;
+  // the tx offsets when the kernel builds the index rows of its inputs' txs
+  // itself (the block kernel, txc_fill: no index launch); null: txt holds them
+  const uint32_t* tx_off;
 };
 // the standard-input lane prologue (1e) run at the head of the mid-size
 // ecmult kernel's lane (defined below, after the std parse helpers)
@@ -1280,18 +1283,39 @@ template <bool STD> struct TxCacheOf { using type = TxCache; };
 template <> struct TxCacheOf<false> { using type = uint32_t; };
 constexpr long long TXC_NONE = -(1ll << 62);
 
+// input c's view (after the barrier that follows txc_fill)
+HKV_DEV TxView txc_view(const TxCache& tc, uint32_t c) {
+  TxView v;
+  const long long d = tc.tx_d[c];
+  const uint32_t b = tc.spk_b[c];
+  // v.t lies outside the LDS object (only v.t + off, off in the tx, lands in
+  // it), so it is formed on the 64-bit flat address as an integer: pointer
+  // arithmetic would let the compiler move the subtraction into the 32-bit
+  // LDS address space, where it wraps
+  const uintptr_t g = reinterpret_cast<uintptr_t>(static_cast<const void*>(&tc.tx[c][0]));
+  v.t = d != TXC_NONE ? reinterpret_cast<const uint8_t*>(g - (uintptr_t)d) : nullptr;
+  v.s = b != ~0u ? reinterpret_cast<const uint8_t*>(&tc.spk[c][0]) + b : nullptr;
+  return v;
+}
 HKV_DEV void txc_fill(TxCache& tc, const StdArgs& sa, uint32_t base, uint32_t n) {
   const uint32_t c = threadIdx.x >> 4, k = threadIdx.x & 15u;  // 16 threads per input
   const uint32_t jx = base + c;
-  uint32_t st = 0, len = 0, so = 0, sl = 0;
+  uint32_t st = 0, len = 0, so = 0, sl = 0, t = ~0u;
   bool sok = false;
   if (jx < n) {
     const hkv_input_job jb = sa.jobs[jx];
     if (jb.tx < sa.n_tx) {
-      const uint32_t* row = sa.txt + (size_t)jb.tx * TXT_WORDS;
-      if (row[TXT_FLAGS] & TXF_OK) {
-        st = row[TXT_START];
-        len = row[TXT_LOCK] + 4u - st;
+      if (sa.tx_off != nullptr) {  // the whole wire form; its row is built below
+        t = jb.tx;
+        st = sa.tx_off[t];
+        const uint32_t e = sa.tx_off[t + 1];
+        len = e >= st ? e - st : 0u;
+      } else {
+        const uint32_t* row = sa.txt + (size_t)jb.tx * TXT_WORDS;
+        if (row[TXT_FLAGS] & TXF_OK) {
+          st = row[TXT_START];
+          len = row[TXT_LOCK] + 4u - st;
+        }
       }
     }
     sok = jb.script_off <= sa.scripts_len && sa.scripts_len - jb.script_off >= jb.script_len && jb.script_len != 0;
@@ -1318,20 +1342,21 @@ HKV_DEV void txc_fill(TxCache& tc, const StdArgs& sa, uint32_t base, uint32_t n)
     tc.tx_d[c] = tfit ? (long long)(pa - reinterpret_cast<uintptr_t>(sa.txs)) : TXC_NONE;
     tc.spk_b[c] = sfit ? (uint32_t)(q0 - qa) : ~0u;
   }
-}
-// input c's view (after the barrier that follows txc_fill)
-HKV_DEV TxView txc_view(const TxCache& tc, uint32_t c) {
-  TxView v;
-  const long long d = tc.tx_d[c];
-  const uint32_t b = tc.spk_b[c];
-  // v.t lies outside the LDS object (only v.t + off, off in the tx, lands in
-  // it), so it is formed on the 64-bit flat address as an integer: pointer
-  // arithmetic would let the compiler move the subtraction into the 32-bit
-  // LDS address space, where it wraps
-  const uintptr_t g = reinterpret_cast<uintptr_t>(static_cast<const void*>(&tc.tx[c][0]));
-  v.t = d != TXC_NONE ? reinterpret_cast<const uint8_t*>(g - (uintptr_t)d) : nullptr;
-  v.s = b != ~0u ? reinterpret_cast<const uint8_t*>(&tc.spk[c][0]) + b : nullptr;
-  return v;
+  if (sa.tx_off != nullptr) {
+    // the index row of each input's tx (hkv_tx_index_kernel's bounds-checked
+    // parse, from the copy when the tx fits), into txt for this group's
+    // readers (after the caller's barrier), the multisig scan and the tail
+    // kernel; inputs of one tx write the same row
+    __syncthreads();
+    if (k == 0 && t != ~0u) {
+      const TxView v = txc_view(tc, c);
+      uint32_t row[8];
+      tx_index_row(v.t != nullptr ? v.t : sa.txs, sa.tx_off, t, row);
+      uint32_t* w = const_cast<uint32_t*>(sa.txt) + (size_t)t * TXT_WORDS;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[q] = row[q];
+    }
+  }
 }
 template <bool STD, class C>
 HKV_DEV TxView blk_view(const C& tc, uint32_t c) {
@@ -2538,13 +2563,15 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
                                    uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, uint32_t n_pad,
                                    int32_t forkid, uint8_t* recs, uint32_t* im, const uint32_t* gtab, uint32_t* qs,
                                    uint32_t* aux, uint32_t* bits, uint32_t n_words, unsigned long long* clk,
-                                   uint32_t n_cu, const MsScan* ms, hipStream_t st) {
-  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr};
+                                   uint32_t n_cu, const MsScan* ms, const uint32_t* tx_off, hipStream_t st) {
+  StdArgs sa{txs, n_tx, txt, scripts, scripts_len, jobs, forkid, nullptr, nullptr, nullptr, nullptr};
   if (ms != nullptr && block_batch(n_pad, n_cu)) {
     sa.ms_desc = ms->desc;
     sa.ms_off = ms->off;
     sa.ms_ctr = reinterpret_cast<unsigned long long*>(ms->counters);
   }
+  if (block_batch(n_pad, n_cu)) sa.tx_off = tx_off;  // the block kernel builds its own rows
+  else if (tx_off != nullptr) return hipErrorInvalidValue;  // the pair kernel reads prebuilt rows
   uint32_t* rw = reinterpret_cast<uint32_t*>(recs);
   if (block_batch(n_pad, n_cu))
     hipLaunchKernelGGL(hkv_block_kernel<true>, dim3(n_pad / BLK_SIGS), dim3(BLK_TPB), 0, st, im, n, n_pad, gtab, qs,
@@ -2565,7 +2592,7 @@ hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
   return hipGetLastError();
 }
 static StdArgs std_args(const StdOps& o) {
-  return StdArgs{o.txs, o.n_tx, o.txt, o.scripts, o.scripts_len, o.jobs, o.forkid, nullptr, nullptr, nullptr};
+  return StdArgs{o.txs, o.n_tx, o.txt, o.scripts, o.scripts_len, o.jobs, o.forkid, nullptr, nullptr, nullptr, nullptr};
 }
 hipError_t launch_std_ecmult_mid(const StdOps& o, uint32_t* im, uint32_t n, uint32_t n_pad, uint32_t* qs,
                                  uint32_t grid, unsigned long long* clk, hipStream_t st) {

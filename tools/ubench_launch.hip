@@ -22,16 +22,18 @@ constexpr int WG = 256;
 // SCRATCH: a dynamically indexed private array (forces a private segment).
 // BODY: a long run of dependent, non-foldable VALU work executed once per
 // wave (straight-line code the I-cache sees cold on every CU).
-template <bool SCRATCH, int BODY, int WR_KB>
+template <bool SCRATCH, int BODY, int WR_KB, bool BIGREG = false, int LDS_KW = 24>
 __global__ void __launch_bounds__(WG, 1) spin_kernel(uint32_t* out, uint32_t ticks, uint32_t sel,
                                                      unsigned long long* stamps) {
-  __shared__ uint32_t lds[24 * 1024];  // 96 KB
+  __shared__ uint32_t lds[LDS_KW * 1024];  // 96 KB by default
   const uint32_t t = threadIdx.x;
   lds[t] = t * sel;
   __syncthreads();
   const unsigned long long t0 = wall_clock64();
   if (t == 0) stamps[2 * blockIdx.x] = t0;
   uint32_t x = lds[(t + 1) & (WG - 1)] + sel;
+  // BIGREG: claim every arch VGPR and AGPR (the block kernel's 256 + 256)
+  if constexpr (BIGREG) asm volatile("v_mov_b32 v255, 0\n\tv_accvgpr_write_b32 a255, 0" ::: "v255", "a255");
   if constexpr (SCRATCH) {
     volatile uint32_t p[3];
     p[sel % 3] = x;
@@ -55,7 +57,7 @@ __global__ void __launch_bounds__(WG, 1) spin_kernel(uint32_t* out, uint32_t tic
   }
 }
 
-template <bool SCRATCH, int BODY, int WR_KB = 0>
+template <bool SCRATCH, int BODY, int WR_KB = 0, bool BIGREG = false, int LDS_KW = 24>
 int run(const char* name, uint32_t* out, unsigned long long* stamps, int n_wg, hipStream_t st) {
   const int wall_khz = 100000;
   hipEvent_t e0, e1;
@@ -63,13 +65,13 @@ int run(const char* name, uint32_t* out, unsigned long long* stamps, int n_wg, h
   CHECK(hipEventCreate(&e1));
   for (uint32_t us : {0u, 100u, 240u}) {
     const uint32_t ticks = us * (uint32_t)(wall_khz / 1000);
-    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((spin_kernel<SCRATCH, BODY, WR_KB>), dim3(n_wg), dim3(WG), 0, st, out, ticks, 1u, stamps);
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((spin_kernel<SCRATCH, BODY, WR_KB, BIGREG, LDS_KW>), dim3(n_wg), dim3(WG), 0, st, out, ticks, 1u, stamps);
     CHECK(hipStreamSynchronize(st));
     const int reps = 40;
     float best = 1e30f, sum = 0;
     for (int r = 0; r < reps; ++r) {
       CHECK(hipEventRecord(e0, st));
-      hipLaunchKernelGGL((spin_kernel<SCRATCH, BODY, WR_KB>), dim3(n_wg), dim3(WG), 0, st, out, ticks, 1u, stamps);
+      hipLaunchKernelGGL((spin_kernel<SCRATCH, BODY, WR_KB, BIGREG, LDS_KW>), dim3(n_wg), dim3(WG), 0, st, out, ticks, 1u, stamps);
       CHECK(hipEventRecord(e1, st));
       CHECK(hipEventSynchronize(e1));
       float ms;
@@ -107,6 +109,9 @@ int main() {
   if (run<false, 40000>("code_320k", out, stamps, n_wg, st)) return 1;
   if (run<true, 40000>("scratch_code_320k", out, stamps, n_wg, st)) return 1;
   if (run<false, 0, 8>("write_2mb", out, stamps, n_wg, st)) return 1;
+  if (run<true, 0, 0, true>("scratch_vgpr512", out, stamps, n_wg, st)) return 1;
+  if (run<true, 0, 0, true, 32>("scratch_vgpr512_lds128k", out, stamps, n_wg, st)) return 1;
+  if (run<true, 40000, 8, true, 32>("scratch_vgpr512_lds128k_code_write", out, stamps, n_wg, st)) return 1;
   if (run<false, 0, 64>("write_16mb", out, stamps, n_wg, st)) return 1;
   CHECK(hipFree(out));
   CHECK(hipFree(stamps));
