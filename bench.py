@@ -224,8 +224,8 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
     got = np.unpackbits(words.view(np.uint8), bitorder="little")[:db.n].astype(bool)
     res = {"txs": db.n_tx, "inputs": db.n, "tx_bytes": int(db.d_bytes.numel()),
            "accepted": int(got.sum()), "rejected": int(db.n - got.sum())}
-    # k calls back to back between two events, three times after max(k, 10)
-    # untimed calls; the median. Without the warm-up the first loop after a
+    # k calls back to back between two events, three times after at least
+    # 100 ms of untimed calls; the median. Without the warm-up the first loop after a
     # data set's first call ran slow and each later one faster (configs[0]
     # 268 / 262 / 255 us, the 64,000-tx batch 1,521 / 1,445 / 1,407 us,
     # profiles/r04r_bench_reps.log), where 20 calls in, every timing method
@@ -233,8 +233,16 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
     # call alone: 255-258 and 1,378-1,395 us, tools/block_timing.py,
     # profiles/r04r_block_timing.txt). The reps stay in the line.
     for name, fn in (("total", run), ("extract_sighash", extract)):
-        for _ in range(max(k, 10)):
-            fn()
+        # warm-up: calls for at least 100 ms of wall time (with 20 calls the
+        # three loops still ran 257 / 252 / 250 us on configs[0],
+        # profiles/r04r_ix_bench.log: the clock ramps over tens of ms)
+        t_w = time.perf_counter()
+        while True:
+            for _ in range(max(k, 10)):
+                fn()
+            torch.cuda.synchronize()
+            if time.perf_counter() - t_w > 0.1:
+                break
         reps = []
         for _ in range(3):
             torch.cuda.synchronize()
