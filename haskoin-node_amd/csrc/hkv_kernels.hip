@@ -1012,7 +1012,8 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
   // phases of workgroup 0 overwrite three of the block kernel's phase slots;
   // 1: lo_table = BIP143 per-tx hashes, digits = sighash, key_sqrt = u1;
   // 2 (sig_wave_parse): lo_table = the input parse, digits = wave 0's key
-  // point, key_sqrt = s^-1, u2 and the digits
+  // point, key_sqrt = s^-1, u2 and the digits; 3 (the block kernel's wave 3):
+  // digits = Q1 received, lo_table = Q1's table built
 #if HKV_SIG_STAMPS == 1
   auto smark = [&](int slot) {
     if (sclk != nullptr && (threadIdx.x & 63) == 0) sclk[4 + slot] = wall_clock64();
@@ -1032,7 +1033,13 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
     if constexpr (SPREAD > 0)  // every input that may sign with the BIP143 form
       bip143_tx_hashes_spread(sa.txs, x.row, x.ok && (x.segwit || sa.forkid >= 0), r32 + 8, shabuf, SPREAD, x.T);
     smark(1);
+#if HKV_EXP_SIGWAVE == 1  // measurement build only (wrong verdicts): no script checks / sighash
+    const bool live = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = 0;
+#else
     const bool live = std_hash(x, sa.txs, sa.forkid, r32, shabuf, d, r32 + 8, SPREAD != 0);
+#endif
     smark(2);
     if (on) {
       if (i < n) std_write_record(r32, x, live, d);  // the input's verify record (hkv_std_input_kernel's)
@@ -1048,7 +1055,14 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
   smark(8);
   gej A;
   bool ainf;
+#if HKV_EXP_SIGWAVE == 2  // measurement build only (wrong verdicts): no u1 G
+  fe_set_u32(A.x, 1);
+  fe_set_u32(A.y, 1);
+  fe_set_u32(A.z, 1);
+  ainf = true;
+#else
   gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
+#endif
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     aux[(size_t)(AUX_AX + k) * n_pad + i] = A.x.v[k];
@@ -1500,6 +1514,12 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       continue;
     }
     // ---- chain waves 0, 1, 3: lanes 0-31 k1, 32-63 k2 (two lanes per chain) ----
+#if HKV_CHAIN_PRIO
+    // the chain waves ahead of the signature wave at the CU's shared units
+    // (measurement knob: the windows run ~1.5x slower while the signature
+    // wave hashes and gathers G-table entries)
+    __builtin_amdgcn_s_setprio(HKV_CHAIN_PRIO);
+#endif
     const int half = (int)(ln >> 5);
     const uint32_t c = (ln & 31u) >> 1;
     const uint32_t i = base + c;
@@ -1555,12 +1575,18 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       blk_post(&bflag[BF_Y], seq);
       mark(STAMP_SQRT);
       blk_wait(&bflag[BF_Q], seq);  // Q1 from wave 1
+#if HKV_SIG_STAMPS == 3
+      if (stamp) clk[4 + STAMP_P] = wall_clock64();
+#endif
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         P.v[k] = qpub[odd ? 1 : 0][k][c];
         zb.v[k] = qpub[2][k][c];
       }
       pair_table(P, half, odd, qlds[2], hlds[2], ln, Zg);
+#if HKV_SIG_STAMPS == 3
+      if (stamp) clk[4 + STAMP_TABLE0] = wall_clock64();
+#endif
     }
     blk_wait(&bflag[BF_SIG], seq);  // the digits, r and flags are in im
     if (wv == 0) mark(STAMP_P);
