@@ -1120,6 +1120,9 @@ HKV_DEV void pair_group(uint32_t base, uint32_t* __restrict__ im, uint32_t n, ui
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
+#ifndef HKV_CHAIN_PRIO
+#define HKV_CHAIN_PRIO 3
+#endif
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
     if (stamp) clk[4 + slot] = wall_clock64();
@@ -1469,6 +1472,9 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
+#ifndef HKV_CHAIN_PRIO
+#define HKV_CHAIN_PRIO 3
+#endif
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
 #if HKV_SIG_STAMPS
@@ -1515,9 +1521,9 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     }
     // ---- chain waves 0, 1, 3: lanes 0-31 k1, 32-63 k2 (two lanes per chain) ----
 #if HKV_CHAIN_PRIO
-    // the chain waves ahead of the signature wave at the CU's shared units
-    // (measurement knob: the windows run ~1.5x slower while the signature
-    // wave hashes and gathers G-table entries)
+    // the chain waves ahead of the signature wave wherever the CU arbitrates
+    // between waves (same box, three runs: configs[0] 246.7 -> 244.5 /
+    // 244.6 us, configs[2] 248.7 -> 246.6 / 247.3 us, profiles/r04r_prio/)
     __builtin_amdgcn_s_setprio(HKV_CHAIN_PRIO);
 #endif
     const int half = (int)(ln >> 5);
