@@ -1055,11 +1055,15 @@ HKV_DEV void sig_wave_gsum(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uint
   smark(8);
   gej A;
   bool ainf;
-#if HKV_EXP_SIGWAVE == 2  // measurement build only (wrong verdicts): no u1 G
-  fe_set_u32(A.x, 1);
-  fe_set_u32(A.y, 1);
-  fe_set_u32(A.z, 1);
-  ainf = true;
+#if HKV_EXP_SIGWAVE == 2  // measurement build only (wrong STD verdicts): no u1 G on standard inputs
+  if constexpr (STD) {
+    fe_set_u32(A.x, 1);
+    fe_set_u32(A.y, 1);
+    fe_set_u32(A.z, 1);
+    ainf = true;
+  } else {
+    gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
+  }
 #else
   gsum_lane(im, n_pad, gtab, i, (flags & FLAG_VALID) != 0, A, ainf);
 #endif
