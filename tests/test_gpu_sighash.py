@@ -271,6 +271,45 @@ def test_std_inputs_block_kernel_small_batches(torch, ver, coracle, forkid):
     assert got == expect
 
 
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_block_kernel_large_txs_vs_oracle(torch, ver, coracle, forkid):
+    """The block kernel copies each input's tx to LDS when it fits in 2 KB
+    (hkv_kernels.hip TxCache, TXC_WORDS) and builds the tx index rows itself;
+    larger txs are parsed, indexed and hashed from HBM. A block of 24-, 14-
+    and 2-input txs (the 24-input ones past 2 KB, the 14-input ones around
+    it) verifies like the oracle through both entry points, and a flipped
+    signature byte in a large tx rejects exactly that input."""
+    import hkv
+    rng = random.Random(5150 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(8)]
+    txs, jobs = txgen.std_block(rng, 6, keys, forkid=forkid, p2wpkh_share=0.3, p2pk_share=0.2, p2sh_share=0.2,
+                                nin_choices=(24, 14, 2))
+    raw = [sh.tx_serialize(t) for t in txs]
+    assert max(len(r) for r in raw) > 2048
+    parsed = [sh.tx_parse(t) for t in raw]
+    exp = b"".join(sh.std_input_record(parsed[t], i, p, v, forkid) for (t, i, p, v) in jobs)
+    want = oracle_batch(coracle, exp, 1).tolist()
+    assert all(want) and len(jobs) <= 4096
+    assert hkv.verify_std_inputs(ver, raw, jobs, forkid) == want
+    assert _device_verify_std(torch, ver, raw, jobs, forkid) == want
+    # flip one signature byte of an input of the largest tx
+    big = max(range(len(raw)), key=lambda k: len(raw[k]))
+    t, i, p, v = next(j for j in jobs if j[0] == big and j[1] == 7)
+    tx = sh.tx_parse(raw[t])
+    if tx.witness and tx.witness[i]:
+        w = list(tx.witness[i])
+        w[0] = w[0][:7] + bytes([w[0][7] ^ 0x10]) + w[0][8:]
+        tx.witness[i] = w
+    else:
+        items = sh._push_items(tx.inputs[i].script)
+        items[0] = items[0][:7] + bytes([items[0][7] ^ 0x10]) + items[0][8:]
+        tx.inputs[i].script = b"".join(txgen.push(x) for x in items)
+    bad = list(raw)
+    bad[t] = sh.tx_serialize(tx)
+    got = _device_verify_std(torch, ver, bad, jobs, forkid)
+    assert got == [not (jt == t and ji == i) for (jt, ji, _, _) in jobs]
+
+
 def test_std_inputs_bip143_example(ver):
     import hkv
     b = json.load(open(os.path.join(GOLDEN, "bip143_p2wpkh.json")))

@@ -82,15 +82,16 @@ def push(data: bytes) -> bytes:
 
 
 def std_block(rng: random.Random, n_tx: int, keys: List[Key], forkid: Optional[int] = None,
-              p2wpkh_share: float = 0.6, p2pk_share: float = 0.0, p2sh_share: float = 0.0):
-    """A synthetic block mix: every tx spends 1-3 standard prevouts (P2WPKH /
-    P2PKH / P2PK / P2SH-P2WPKH) and pays 2 outputs, SIGHASH_ALL (| FORKID on a fork-id
-    network). Returns (txs, jobs) with jobs = [(tx index, input, prevout
-    script, value)]."""
+              p2wpkh_share: float = 0.6, p2pk_share: float = 0.0, p2sh_share: float = 0.0,
+              nin_choices=(1, 1, 2, 2, 3)):
+    """A synthetic block mix: every tx spends 1-3 (nin_choices) standard
+    prevouts (P2WPKH / P2PKH / P2PK / P2SH-P2WPKH) and pays 2 outputs,
+    SIGHASH_ALL (| FORKID on a fork-id network). Returns (txs, jobs) with
+    jobs = [(tx index, input, prevout script, value)]."""
     txs, jobs = [], []
     shbyte = 0x41 if forkid is not None else 0x01
     for t in range(n_tx):
-        nin = rng.choice([1, 1, 2, 2, 3])
+        nin = rng.choice(list(nin_choices))
         kinds, ks, vals = [], [], []
         ins = []
         for _ in range(nin):
