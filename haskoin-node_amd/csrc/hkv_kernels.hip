@@ -1124,9 +1124,6 @@ HKV_DEV void pair_group(uint32_t base, uint32_t* __restrict__ im, uint32_t n, ui
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
-#ifndef HKV_CHAIN_PRIO
-#define HKV_CHAIN_PRIO 3
-#endif
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
     if (stamp) clk[4 + slot] = wall_clock64();
@@ -1276,6 +1273,9 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
 // 1's doublings start 6 us earlier; profiles/r04r_blk_k/summary.txt): was (18, 28)
 #ifndef HKV_BLK_K1
 #define HKV_BLK_K1 17
+#endif
+#ifndef HKV_CHAIN_PRIO  // the block kernel's chain waves' issue priority (s_setprio; 0: off)
+#define HKV_CHAIN_PRIO 3
 #endif
 #ifndef HKV_BLK_K2
 #define HKV_BLK_K2 27
@@ -1476,9 +1476,6 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
   const uint32_t odd = (ln & 1u) ? 0xFFFFFFFFu : 0u;
-#ifndef HKV_CHAIN_PRIO
-#define HKV_CHAIN_PRIO 3
-#endif
   const bool stamp = clk != nullptr && blockIdx.x == 0 && ln == 0;
   auto mark = [&](int slot) {
 #if HKV_SIG_STAMPS
