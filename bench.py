@@ -33,14 +33,14 @@ algorithm's limb products per verify, hkv/opcount.py P_ALG_ECMULT, over the
 HIP-event-timed ecmult + finish launches, against the v_mad_u64_u32 peak at 2.4 GHz and at the
 measured mad rate and clock); configs[0] (the 2,000-tx P2PKH block), [2]
 (block mix) and [3] (adversarial 1M, every class of hkv/adversarial.py); and
-the CPU baseline leg: a restatement of libsecp256k1's verify algorithm
-(oracle/secp_fast.c: GLV, w = 15 G tables, safegcd — the reference library's
-class), the plain C restatement (oracle/hkv_oracle.c) — both kind "port" — and
-OpenSSL's ECDSA_do_verify (the survey's labelled non-reference fallback;
-libsecp256k1 is not installed on the box), single-thread and over a thread sweep (1, 16, 64,
-128 and the affinity count; the cgroup CPU quota is recorded), on the
-configs[0] block and on config-2 / adversarial samples, with their verdicts
-compared to the GPU's on the same records.
+the CPU baseline leg: oracle/secp_fast.c, a restatement of libsecp256k1's
+verify algorithm (GLV, w = 15 G tables, safegcd — the reference library's
+class; libsecp256k1 is not installed on the box), timed in steady state (every
+point >= 1 s of wall time, CPU seconds recorded) over a thread sweep (1, 16,
+64, 128 and the affinity count) under the job's cgroup CPU quota, beside the
+plain C restatement (oracle/hkv_oracle.c) and OpenSSL's ECDSA_do_verify; the
+whole-host rate is extrapolated from the per-core rate and the host's
+physical cores, and the north_star ratio is reported against both.
 """
 from __future__ import annotations
 
@@ -117,24 +117,69 @@ def thread_sweep() -> list:
     return sorted({t for t in (1, 16, 64, 128, aff) if t <= max(1, min(aff, 256))} | {min(aff, 256)})
 
 
-def cpu_baseline(samples, sweep) -> dict:
+def physical_cores(info: dict):
+    """Physical cores of the whole host (lscpu sockets x cores per socket)."""
+    try:
+        return int(info["Socket(s)"]) * int(info["Core(s) per socket"])
+    except (KeyError, ValueError):
+        return None
+
+
+def cpu_seconds() -> float:
+    """CPU time (user + system) of this process, every thread included."""
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
+
+
+def steady_rate(fn, recs, mode: int, threads: int, min_s: float, per_thread: int = 2000) -> dict:
+    """Records/s of fn(records, n, mode, out, threads) in steady state: calls
+    on `per_thread` records per thread (the sample tiled) repeated until at
+    least min_s of wall time has passed — >= 10 periods of the cgroup's CFS
+    quota, so a burst at the start of a period cannot inflate the rate — with
+    the process's CPU seconds recorded beside the wall clock (per-core rate =
+    records / CPU-s)."""
+    import numpy as np
+    n0 = len(recs) // 168
+    m = max(n0, per_thread * threads)
+    reps = -(-m // n0)
+    buf = np.ascontiguousarray(np.tile(recs, reps)[: m * 168] if reps > 1 else recs)
+    out = np.zeros(m, dtype=np.uint8)
+    done, calls = 0, 0
+    c0, t0 = cpu_seconds(), time.perf_counter()
+    while True:
+        fn(ctypes.c_void_p(buf.ctypes.data), m, mode, ctypes.c_void_p(out.ctypes.data), threads)
+        done += m
+        calls += 1
+        wall = time.perf_counter() - t0
+        if wall >= min_s:
+            break
+    cpu = cpu_seconds() - c0
+    return {"threads": threads, "records": done, "calls": calls, "wall_s": round(wall, 3), "cpu_s": round(cpu, 3),
+            "rate": round(done / wall, 1), "per_cpu_s": round(done / cpu, 1) if cpu > 0 else None,
+            "verdicts": out[:n0].astype(bool)}
+
+
+def cpu_baseline(samples, sweep, min_s: float = 1.0) -> dict:
     """The CPU leg (oracle/ is timed here and used as the checker here only).
 
     samples: [(name, records uint8 [n*168], mode, gpu verdicts bool[n] or None)].
-    The first sample (configs[0]'s block) is timed at every thread count of
-    `sweep` for each implementation, tiled to 1,500 records per thread (at
-    least the block) so every thread has ~0.15 s of work; `value` is the best
-    rate of the sweep and `cores` the thread count that reached it. The other
-    samples are timed on 1 thread (first 4,096 records) and at that thread
-    count; every sample's verdicts are compared with the GPU's.
-    Implementations: "secpfast" = oracle/secp_fast.c, a restatement of
-    libsecp256k1's verify algorithm (5x52 field, GLV + wNAF5 Strauss, w = 15
-    G tables, variable-time safegcd s^-1: the reference library's class, so
-    north_star's "x the all-core host libsecp256k1 rate" can be judged);
-    "port" = oracle/hkv_oracle.c (C restatement of the reference semantics;
-    no GLV, generic inversions); "openssl" = OpenSSL 3 ECDSA_do_verify behind
-    the semantic adapter (oracle/openssl_check.c) — the survey's labelled
-    non-reference fallback. libsecp256k1 itself is absent on the box."""
+    Every timed point is a steady-state measurement (steady_rate: >= min_s of
+    wall time, CPU seconds recorded). The reported baseline is "secpfast" =
+    oracle/secp_fast.c, a restatement (port) of libsecp256k1's verify
+    algorithm (5x52 field, GLV + wNAF5 Strauss, w = 15 G tables,
+    variable-time safegcd s^-1) — the reference library's class; the library
+    itself is not installed on the box. It is timed on the first sample
+    (configs[0]'s block) at every thread count of `sweep`; `value` is the best
+    steady rate (bound by the job's cgroup CPU quota) and `cores` the thread
+    count that reached it. Beside it: "port" = oracle/hkv_oracle.c (plain C
+    restatement; no GLV, generic inversions) and "openssl" = OpenSSL 3
+    ECDSA_do_verify behind oracle/openssl_check.c (the survey's labelled
+    non-reference fallback), each at 1 thread and at the quota's CPU count.
+    The other samples are timed with secpfast at 1 thread; every
+    implementation's verdicts on every sample are compared with the GPU's.
+    The whole-host rate is an extrapolation: the per-core rate (records per
+    CPU-second) x the host's physical cores (lscpu)."""
     import numpy as np
     import subprocess
     ob = os.path.join(ROOT, "oracle", "build")
@@ -150,59 +195,94 @@ def cpu_baseline(samples, sweep) -> dict:
     fast.hkvo_fast_verify_batch.argtypes = argt
     impls = {"secpfast": fast.hkvo_fast_verify_batch, "port": port.hkvo_verify_batch,
              "openssl": ossl.hkvo_openssl_verify_batch}
+    host = host_info()
+    quota = host.get("cgroup", {}).get("quota_cpus")
+    aff = host.get("affinity_cpus") or os.cpu_count() or 1
+    q_threads = max(1, min(aff, int(quota) if quota else aff, 256))
 
-    def run(fn, recs, mode, t):
-        n = len(recs) // 168
-        out = np.zeros(n, dtype=np.uint8)
-        t0 = time.perf_counter()
-        fn(ctypes.c_void_p(recs.ctypes.data), n, mode, ctypes.c_void_p(out.ctypes.data), t)
-        return n / (time.perf_counter() - t0), out.astype(bool)
+    def point(fn, recs, mode, t):
+        r = steady_rate(fn, recs, mode, t, min_s)
+        v = r.pop("verdicts")
+        return r, v
 
     res = {}
-    best = (0.0, "port", 1)  # (rate, impl, threads) on the first sample
+    best = None  # secpfast on the first sample: (rate, threads)
+    single = per_core = None
     for si, (name, recs, mode, gpu) in enumerate(samples):
         recs = np.ascontiguousarray(recs)
         n = len(recs) // 168
         row = {"records": n, "mode": "LIBSECP" if mode == 0 else "HASKOIN"}
-        n1 = min(n, 4096)  # single-thread run: the first 4,096 records
         for iname, fn in impls.items():
-            st, _ = run(fn, recs[: n1 * 168], mode, 1)
-            r = {"1_thread": round(st, 1)}
-            counts = [t for t in sweep if t > 1] if si == 0 else [best[2]] if best[2] > 1 else []
+            if si == 0:
+                counts = sweep if iname == "secpfast" else sorted({1, q_threads})
+            else:
+                counts = [1] if iname == "secpfast" else []
+            r = {}
             vm = None
             for t in counts:
-                reps = max(1, -(-1500 * t // n))
-                mt, v = run(fn, np.tile(recs, reps) if reps > 1 else recs, mode, t)
-                r[f"{t}_threads"] = round(mt, 1)
-                vm = v[:n] if vm is None else vm
-                if si == 0 and mt > best[0]:
-                    best = (mt, iname, t)
-            if si == 0 and st > best[0]:
-                best = (st, iname, 1)
-            if vm is None:
-                _, vm = run(fn, recs, mode, 1)
+                pt, v = point(fn, recs, mode, t)
+                r[f"{t}_threads"] = pt
+                vm = v if vm is None else vm
+                if si == 0 and iname == "secpfast":
+                    if best is None or pt["rate"] > best[0]:
+                        best = (pt["rate"], t)
+                    if t == 1:
+                        single, per_core = pt["rate"], pt["per_cpu_s"]
+            if vm is None:  # verdicts only (untimed)
+                out = np.zeros(n, dtype=np.uint8)
+                fn(ctypes.c_void_p(recs.ctypes.data), n, mode, ctypes.c_void_p(out.ctypes.data), q_threads)
+                vm = out.astype(bool)
             r["accepts"] = int(vm.sum())
             if gpu is not None:
                 r["mismatches_vs_gpu"] = int((vm != gpu).sum())
             row[iname] = r
         res[name] = row
-    first = samples[0][0] if samples else None
-    rate, impl, cores = best
-    return {"value": round(rate, 1) if first else None, "unit": "verifies/s", "cores": cores,
-            "kind": "port",
-            "impl": impl,
-            "impl_note": {"secpfast": "oracle/secp_fast.c: libsecp256k1's verify algorithm restated (5x52 field, "
-                                      "GLV + wNAF5, w=15 G tables, safegcd), incl. the pubkey parse / sqrt",
-                          "port": "oracle/hkv_oracle.c: plain restatement (no GLV, Fermat inversions)",
-                          "openssl": "OpenSSL 3 ECDSA_do_verify behind oracle/openssl_check.c"},
+    if not samples:
+        return {"value": None, "unit": "verifies/s", "cores": None, "kind": "port", "impl": "secpfast"}
+    rate, cores = best
+    phys = physical_cores(host)
+    first = samples[0][0]
+    top = res[first]["secpfast"][f"{cores}_threads"]
+    return {"value": rate, "unit": "verifies/s", "cores": cores, "kind": "port", "impl": "secpfast",
+            "kind_note": "a port of the reference library's algorithm: oracle/secp_fast.c restates libsecp256k1's "
+                         "verify (5x52 field, GLV + wNAF5, w=15 G tables, safegcd, the pubkey parse / sqrt); "
+                         "libsecp256k1 itself is not installed on the box and not in /root/reference",
             "sample": f"BASELINE configs[0]: the 4,000 inputs of the 2,000-tx P2PKH block (records extracted on "
-                      f"device, HKV_HASKOIN = verifyHashSig), tiled to 1,500 records per thread; best of the "
-                      f"libsecp256k1-class restatement (secpfast), the plain C restatement (port) and OpenSSL "
-                      f"ECDSA_do_verify over the thread sweep {list(sweep)} (value at cores = {cores} threads); "
-                      f"libsecp256k1 itself is not installed on the box",
-            "thread_sweep": list(sweep),
-            "single_thread_value": res.get(first, {}).get(impl, {}).get("1_thread") if first else None,
-            "samples": res, "host": host_info()}
+                      f"device, HKV_HASKOIN = verifyHashSig), tiled to 2,000 records per thread per call, each "
+                      f"point repeated for >= {min_s:g} s of wall time; value = the best steady rate of the thread "
+                      f"sweep {list(sweep)} (cores = {cores}), bound by this job's cgroup CPU quota "
+                      f"({quota} CPUs)",
+            "single_thread_value": single,
+            "per_core_value": per_core,
+            "per_core_note": "records per CPU-second (getrusage) of the 1-thread point",
+            "quota_cpus": quota,
+            "quota_bound_value": rate,
+            "quota_check": {"max_point": top["rate"], "bound": round(quota * single * 1.1, 1) if quota and single
+                            else None,
+                            "ok": bool(top["rate"] <= quota * single * 1.1) if quota and single else None,
+                            "note": "no sweep point may exceed quota x single-thread rate x 1.1 (steady state)"},
+            "whole_host": {"physical_cores": phys,
+                           "extrapolated_value": round(per_core * phys, 1) if per_core and phys else None,
+                           "note": "per_core_value x the host's physical cores (lscpu): an extrapolation, not a "
+                                   "measurement (the job may use only its cgroup quota)"},
+            "thread_sweep": list(sweep), "samples": res, "host": host}
+
+
+def north_star_ratio(value: float, cpu: dict) -> dict:
+    """north_star: ">= 50x the all-core host libsecp256k1 verify rate on one
+    MI355X". The whole-host figure is the extrapolation (per-core rate x
+    physical cores); the quota-bound figure is what this job measured."""
+    wh = (cpu.get("whole_host") or {}).get("extrapolated_value")
+    out = {"whole_host_extrapolated": round(value / wh, 1) if wh else None,
+           "quota_bound": round(value / cpu["value"], 1) if cpu.get("value") else None,
+           "single_thread": round(value / cpu["single_thread_value"], 1) if cpu.get("single_thread_value") else None,
+           "target": 50.0}
+    out["target_met_whole_host"] = bool(out["whole_host_extrapolated"] >= 50.0) \
+        if out["whole_host_extrapolated"] is not None else None
+    out["note"] = ("value (configs[1], HBM-resident) / the CPU rates: whole_host_extrapolated is the north_star "
+                   "reading (all host cores, extrapolated from the per-core rate); quota_bound is against this "
+                   "job's cgroup CPU share (measured)")
+    return out
 
 
 def _time_block(v, torch, db, bstream, k: int) -> dict:
@@ -280,9 +360,11 @@ def _time_block(v, torch, db, bstream, k: int) -> dict:
                              "enqueue_us_per_block": round(t_enq / 32 * 1e6, 1),
                              "note": "32 calls of hkv_verify_std_inputs_device on one stream, no host sync between "
                                      "them; host wall clock from the first enqueue to the last verdict"}
-    # (a block: one workgroup of the block kernel per 16 inputs)
+    # (a block: one workgroup of the block kernel per 16 inputs). Other batch
+    # sizes run other kernels, which leave no fresh stamps: null
     n_pad = (db.n + 255) // 256 * 256
-    res["split_phases_us"] = split_phases(v, torch, run, n_pad // 16 if n_pad <= 16 * 256 else 0)
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    res["split_phases_us"] = split_phases(v, torch, run, n_pad // 16) if n_pad <= 16 * n_cu else None
     return res, got
 
 
@@ -304,6 +386,12 @@ def split_phases(v, torch, run, n_groups: int = 0) -> dict:
     tick = ctypes.c_double()
     v.lib.hkv_profile_phases(v.ctx, 0, stamps, len(PHASES), ctypes.byref(tick))
     out = {name: round((int(stamps[k]) - int(stamps[0])) * tick.value * 1e-3, 1) for k, name in enumerate(PHASES)}
+    # every stamp of this call lies after its start and within the call: a
+    # stamp outside that was not written by it
+    bad = [name for name in PHASES if not 0.0 <= out[name] < 1e5]
+    if bad:
+        v.lib.hkv_profile_enable(v.ctx, 0)
+        return {"error": f"stale or missing phase stamps: {bad}"}
     # every workgroup's (start, end) stamps (the block kernel only): how far
     # the launch's span reaches beyond workgroup 0's phase stamps
     if n_groups and hasattr(v.lib, "hkv_profile_group_stamps"):
@@ -630,14 +718,37 @@ def _free_port() -> int:
 
 
 def visible_devices() -> int:
-    """GPUs this process may use. torch.cuda.device_count() does not
-    initialise the GPU on this image, so the launcher may call it before it
-    starts the ranks."""
-    import torch
-    return torch.cuda.device_count()
+    """GPUs this process may use, counted without HIP (the launcher parent
+    starts the ranks by fork + exec and must not have touched the GPU first):
+    the KFD topology's GPU nodes (non-zero gpu_id) whose render node this
+    process can open (a device cgroup refuses the others), then the
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES filters."""
+    import glob
+    n = 0
+    for node in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*")):
+        try:
+            if int(open(os.path.join(node, "gpu_id")).read().strip() or 0) == 0:
+                continue
+            minor = None
+            for line in open(os.path.join(node, "properties")):
+                k, _, val = line.partition(" ")
+                if k == "drm_render_minor":
+                    minor = int(val)
+            if minor is None:
+                continue
+            fd = os.open(f"/dev/dri/renderD{minor}", os.O_RDWR | os.O_CLOEXEC)
+            os.close(fd)
+            n += 1
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = os.environ.get(var)
+        if val is not None:
+            n = min(n, len([x for x in val.split(",") if x.strip()]))
+    return n
 
 
-def spawn_ranks(n: int, argv: list, mock: bool = False) -> int:
+def spawn_ranks(n: int, argv: list, mock: bool = False, share_device: bool = False) -> int:
     """`python bench.py --gpus N` without a launcher: start N rank processes
     (fresh interpreters, never an exec of this one) with RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* set as torchrun would, wait for all of them and
@@ -647,7 +758,7 @@ def spawn_ranks(n: int, argv: list, mock: bool = False) -> int:
     import subprocess
     if not mock:
         have = visible_devices()
-        if n > have:
+        if (1 if share_device else n) > have:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
             return 2
     port = _free_port()
@@ -760,12 +871,16 @@ def main() -> None:
                     help="BASELINE configs[4] (16,777,216 records, 5%% invalid, seed 0x484B5635, sharded over the "
                          "ranks); the default whenever WORLD_SIZE > 1")
     ap.add_argument("--config4-n", type=int, default=CONFIG4_N, help=argparse.SUPPRESS)
+    ap.add_argument("--share-device", action="store_true",
+                    help="test only: every rank runs on device 0 (the N > 1 code path on a 1-GPU lease); the "
+                         "verdict words are all-gathered over gloo through host memory, since RCCL takes one rank "
+                         "per GPU. Not a scaling measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
     launched = "WORLD_SIZE" in os.environ
     if not launched and (args.gpus or 1) > 1:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], mock=args.mock_cpu))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], mock=args.mock_cpu, share_device=args.share_device))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -781,16 +896,22 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
+    share = args.share_device
+    gpu = 0 if share else local  # (--share-device: every rank on device 0)
     have = torch.cuda.device_count()
-    if local >= have:
-        print(f"bench.py: rank {rank} needs GPU {local} but only {have} visible", file=sys.stderr, flush=True)
+    if gpu >= have:
+        print(f"bench.py: rank {rank} needs GPU {gpu} but only {have} visible", file=sys.stderr, flush=True)
         sys.exit(2)
+    torch.cuda.set_device(gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    # the tensors the ranks reduce over: on the device for RCCL, in host
+    # memory for gloo
+    red_dev = "cpu" if share else "cuda"
 
     import hkv
     from hkv import opcount
@@ -804,7 +925,7 @@ def main() -> None:
         n_total, seed, inv = args.config4_n, CONFIG4_SEED, CONFIG4_INVALID_PERMILLE
     else:
         n_total, seed, inv = args.per_gpu * world, SEED, 0
-    v = hkv.Verifier(hkv.VerifierConfig(device_ids=[local]))
+    v = hkv.Verifier(hkv.VerifierConfig(device_ids=[gpu]))
     # a real (non-null) stream made current: libhkv enqueues on it and the RCCL
     # all-gather, which waits on torch's current stream, is ordered after the
     # verify (the null stream would not order against libhkv's own stream)
@@ -815,7 +936,7 @@ def main() -> None:
     def verify_shard(lo, hi, bits):
         v.verify_device(0, recs.data_ptr(), hi - lo, args.mode, bits.data_ptr(), sptr)
 
-    sv = ShardedVerify(torch, n_total, rank, world, verify_shard, dist=dist)
+    sv = ShardedVerify(torch, n_total, rank, world, verify_shard, dist=dist, gather_on_host=share)
     n = sv.local_n
     recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
     labels = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
@@ -846,7 +967,7 @@ def main() -> None:
     v.lib.hkv_profile_enable(v.ctx, 0)
 
     t = torch.tensor([dt, em.value / max(1, nl.value), pm.value / max(1, nl.value)], dtype=torch.float64,
-                     device="cuda")
+                     device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max, ecm_ms, pro_ms = t.tolist()
@@ -860,12 +981,12 @@ def main() -> None:
     chk = torch.tensor([sv.slice_mismatches(full, lab_np),
                         int(np.unpackbits(full.view(np.uint8), bitorder="little")[sv.lo:sv.hi].sum()),
                         int(np.unpackbits(lab_np.view(np.uint8), bitorder="little")[:n].sum())],
-                       dtype=torch.int64, device="cuda")
+                       dtype=torch.int64, device=red_dev)
     if world > 1:
         dist.all_reduce(chk, op=dist.ReduceOp.SUM)
     mismatches, accepted, label_valid = chk.tolist()
     # which device every rank ran on (the line proves N ranks on N GPUs)
-    props = torch.cuda.get_device_properties(local)
+    props = torch.cuda.get_device_properties(gpu)
     me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(), "name": props.name,
           "pci_bus_id": getattr(props, "pci_bus_id", None), "pci_device_id": getattr(props, "pci_device_id", None),
           "uuid": str(getattr(props, "uuid", "")) or None, "pid": os.getpid(), "local_n": n}
@@ -918,14 +1039,8 @@ def main() -> None:
                                     adv_recs[: m4 * 168], mode, adv_got[mode][:m4]))
             cpu = cpu_baseline(samples, thread_sweep())
             # north_star: ">= 50x the all-core host libsecp256k1 verify rate"
-            # (here: the job's CPU share, see cpu_baseline.host.cgroup)
             if cpu.get("value"):
-                cpu["gpu_over_cpu"] = {
-                    "all_core": round(value / cpu["value"], 1),
-                    "single_thread": round(value / cpu["single_thread_value"], 1)
-                    if cpu.get("single_thread_value") else None,
-                    "note": "value (configs[1], HBM-resident) / the best CPU rate of the sweep (impl, cores); the "
-                            "CPU figure is the job's cgroup CPU share, not the whole host"}
+                cpu["gpu_over_cpu"] = north_star_ratio(value, cpu)
             if c0_recs is not None:
                 cpu["config0_host_sighash"] = cpu_sighash_leg(c0_txs, c0_inputs, c0_recs)
         if config4:
@@ -943,6 +1058,7 @@ def main() -> None:
             "n_gpus": world,
             "ranks_seen": ranks_seen,
             "rank_devices": rank_devices,
+            "share_device": share,
             "launcher": ("bench.py spawn" if os.environ.get("HKV_BENCH_SPAWNED") else
                          "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or "GROUP_RANK" in os.environ else
                          "external" if world > 1 else "single process"),

@@ -72,7 +72,14 @@ struct DevCtx {
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   void* ms_ctr = nullptr;            // scan counters: [0] running sum (the tail reads and re-arms it)
-  unsigned int* ms_bar = nullptr;    // the tail kernel's grid barrier: [0] arrivals, [1] sense, [2] fault
+  // the tail kernel's words: [0..3] and [4..7] the two grid-barrier slots
+  // (arrivals, sense; launch `tail_epoch` uses slot tail_epoch & 1 and zeroes
+  // the other), [8] the sticky fault latch (hkv_device_fault), [9] the host
+  // form's per-call status word
+  unsigned int* ms_bar = nullptr;
+  uint32_t tail_epoch = 0;
+  bool inject_tail = false;          // hkv_debug_fail_device(HKV_FAIL_TAIL): the next tail launch's barriers give up
+  uint32_t* call_status = nullptr;   // the current call's status word (device; HKV_STATUS_* ORed in), or null
   bool ms_dirty = false;             // a call failed after its scan launch: zero ms_ctr before the next scan
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
   bool rare_dirty = false;           // a finish launch failed part-way: zero rare_ctr before the next one
@@ -146,6 +153,7 @@ size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 constexpr size_t STD_CHUNK = 1u << 17;
 constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
 constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFF00ull;
+constexpr size_t MS_BAR_WORDS = 16, MS_FAULT = 8, MS_HOST_STATUS = 9;  // DevCtx::ms_bar
 
 int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
   if (d.im_cap < n_pad) {
@@ -301,8 +309,8 @@ int init_device(DevCtx& d, int device) {
   // the tail's barrier words
   HKV_TRY(hipMalloc(&d.ms_ctr, 4 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 4 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
-  HKV_TRY(hipMalloc(reinterpret_cast<void**>(&d.ms_bar), 4 * sizeof(unsigned int)), "hipMalloc(multisig barrier)");
-  HKV_TRY(hipMemsetAsync(d.ms_bar, 0, 4 * sizeof(unsigned int), d.stream), "hipMemset(multisig barrier)");
+  HKV_TRY(hipMalloc(reinterpret_cast<void**>(&d.ms_bar), MS_BAR_WORDS * sizeof(unsigned int)), "hipMalloc(multisig barrier)");
+  HKV_TRY(hipMemsetAsync(d.ms_bar, 0, MS_BAR_WORDS * sizeof(unsigned int), d.stream), "hipMemset(multisig barrier)");
   HKV_TRY(hipMalloc(&d.rare_ctr, sizeof(uint32_t)), "hipMalloc(rare counter)");
   HKV_TRY(hipMemsetAsync(d.rare_ctr, 0, sizeof(uint32_t), d.stream), "hipMemset(rare counter)");
   HKV_TRY(hipStreamSynchronize(d.stream), "multisig counters sync");  // callers may use other streams
@@ -608,7 +616,13 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
   t.qs = d.qs;
   t.out_bits = out_bits;
   t.bar = d.ms_bar;
+  t.epoch = d.tail_epoch;
+  t.fault = d.ms_bar + MS_FAULT;
+  t.status = d.call_status;
+  t.force_fault = d.inject_tail ? 1u : 0u;
   HKV_TRY(hkv::launch_ms_tail(t, (uint32_t)d.n_cu, st), "multisig tail launch");
+  ++d.tail_epoch;  // (launched: it zeroes the slot the next launch uses)
+  d.inject_tail = false;
   return HKV_OK;
 }
 
@@ -736,10 +750,28 @@ int hkv_device_failures(hkv_ctx* ctx, int dev) {
 }
 
 int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when) {
-  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || when > HKV_FAIL_ALLOC) return HKV_E_ARG;
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || when > HKV_FAIL_TAIL) return HKV_E_ARG;
   std::lock_guard<std::mutex> lock(ctx->mu);
-  ctx->devs[(size_t)dev].inject = when;
+  if (when == HKV_FAIL_TAIL) ctx->devs[(size_t)dev].inject_tail = true;
+  else ctx->devs[(size_t)dev].inject = when;
   return HKV_OK;
+}
+
+int hkv_device_fault(hkv_ctx* ctx, int dev, uint32_t* fault) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !fault) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[(size_t)dev];
+  HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
+  // after every call enqueued so far on this device (the scratch order), read
+  // then clear the latch
+  unsigned int w = 0;
+  int rc = scratch_acquire(d, d.stream);
+  if (rc) return rc;
+  HKV_TRY(hipMemcpyAsync(&w, d.ms_bar + MS_FAULT, sizeof(w), hipMemcpyDeviceToHost, d.stream), "D2H fault latch");
+  HKV_TRY(hipMemsetAsync(d.ms_bar + MS_FAULT, 0, sizeof(unsigned int), d.stream), "hipMemset(fault latch)");
+  HKV_TRY(hipStreamSynchronize(d.stream), "fault latch sync");
+  *fault = w ? HKV_STATUS_TAIL_FAULT : 0u;
+  return scratch_release(d, d.stream);
 }
 
 int hkv_batch_alloc(hkv_ctx* ctx, size_t max_n, hkv_batch** out) {
@@ -1089,8 +1121,9 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
   return rc;
 }
 
-int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
-                                 int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream) {
+int hkv_verify_std_inputs_device_status(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs,
+                                        size_t n, int32_t forkid, void* d_records, uint32_t* d_bits,
+                                        uint32_t* d_status, void* hip_stream) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !txs_ok(d_txs) || n > HKV_MAX_STD_INPUTS) return HKV_E_ARG;
   if (n == 0) return HKV_OK;
   if (!d_jobs || !d_records || !d_bits) return HKV_E_ARG;
@@ -1100,9 +1133,17 @@ int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, co
   HKV_TRY(hipSetDevice(d.device), "hipSetDevice");
   hipStream_t st = static_cast<hipStream_t>(hip_stream);  // NULL: the null (default) stream (include/hkv.h)
   int rc = scratch_acquire(d, st);
+  d.call_status = d_status;
   if (!rc) rc = enqueue_verify_std_inputs(d, d_txs, d_jobs, n, forkid, d_records, d_bits, st);
+  d.call_status = nullptr;
   if (rc) return rc;
   return scratch_release(d, st);
+}
+
+int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
+                                 int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream) {
+  return hkv_verify_std_inputs_device_status(ctx, dev, d_txs, d_jobs, n, forkid, d_records, d_bits, nullptr,
+                                             hip_stream);
 }
 
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
@@ -1126,16 +1167,20 @@ int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job*
     d.recs_cap = n;
   }
   if (!rc) rc = grow(&d.ms[6], &d.ms_cap[6], (n + 31) / 32 * 4, "hipMalloc(verdict words)");
-  if (!rc)
-    rc = enqueue_verify_std_inputs(d, &dt, static_cast<const hkv_input_job*>(djobs), n, forkid, d.recs,
-                                   static_cast<uint32_t*>(d.ms[6]), d.stream);
+  if (rc) return rc;
+  // this call's status word (a fault of an earlier call is not this call's)
+  uint32_t* status = reinterpret_cast<uint32_t*>(d.ms_bar + MS_HOST_STATUS);
+  HKV_TRY(hipMemsetAsync(status, 0, sizeof(uint32_t), d.stream), "hipMemset(call status)");
+  d.call_status = status;
+  rc = enqueue_verify_std_inputs(d, &dt, static_cast<const hkv_input_job*>(djobs), n, forkid, d.recs,
+                                 static_cast<uint32_t*>(d.ms[6]), d.stream);
+  d.call_status = nullptr;
   if (rc) return rc;
   HKV_TRY(hipMemcpyAsync(verdict_bits, d.ms[6], (n + 31) / 32 * 4, hipMemcpyDeviceToHost, d.stream), "D2H bits");
-  unsigned int fault = 0;
-  HKV_TRY(hipMemcpyAsync(&fault, d.ms_bar + 2, sizeof(fault), hipMemcpyDeviceToHost, d.stream), "D2H tail fault");
+  uint32_t fault = 0;
+  HKV_TRY(hipMemcpyAsync(&fault, status, sizeof(fault), hipMemcpyDeviceToHost, d.stream), "D2H call status");
   HKV_TRY(hipStreamSynchronize(d.stream), "std inputs sync");
-  if (fault) {  // the multisig tail's grid barrier gave up (its verdicts stayed 0): report it once
-    HKV_TRY(hipMemsetAsync(d.ms_bar + 2, 0, sizeof(unsigned int), d.stream), "hipMemset(tail fault)");
+  if (fault & HKV_STATUS_TAIL_FAULT) {  // the multisig tail's grid barrier gave up (its verdicts are incomplete)
     g_last_hip = "multisig tail: grid barrier timed out (workgroups not co-resident)";
     (void)scratch_release(d, d.stream);
     return HKV_E_INTERNAL;

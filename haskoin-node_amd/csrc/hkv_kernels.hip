@@ -2447,12 +2447,22 @@ namespace hkv {
 //          on slot-relative scratch sized by the grid;
 //       4. per input, haskoin's countMulSig over its candidate verdicts
 //          (ms_resolve_lane), ORed into the batch's verdict words.
-//     The grid is one workgroup per CU, so every workgroup is resident at
-//     once on an otherwise idle device; the barrier's spin is bounded anyway
-//     (a workgroup that waits ~seconds gives up: the multisig verdicts then
-//     stay 0 — reject, never a false accept — and bar[2] records the fault).
+//     The grid is one workgroup per CU, launched cooperatively (HKV_TAIL_COOP:
+//     hipLaunchCooperativeKernel fails rather than start a grid whose
+//     workgroups cannot all be resident), so the barriers cannot starve.
+//     Their spin is bounded anyway: a workgroup that waits ~seconds gives up,
+//     the multisig verdicts it owns stay 0 (reject, never a false accept: a
+//     barrier releases only when every workgroup has arrived, i.e. has
+//     finished the phase before it), and the fault is reported through the
+//     device's sticky latch and the call's status word (HKV_STATUS_TAIL_FAULT).
+//     Each launch uses its own barrier slot (the epoch's parity) and zeroes
+//     the other one for the next launch, so a faulted launch's leftover
+//     arrivals can never release a later launch's barrier early.
 // ---------------------------------------------------------------------------
-HKV_DEV bool grid_sync(unsigned int* bar, unsigned int& sense, uint32_t* lds_flag) {
+#ifndef HKV_TAIL_COOP  // the multisig tail by hipLaunchCooperativeKernel (0: a plain launch)
+#define HKV_TAIL_COOP 1
+#endif
+HKV_DEV bool grid_sync(const MsTail& a, unsigned int* bar, unsigned int& sense, uint32_t* lds_flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
     sense ^= 1u;
@@ -2463,14 +2473,17 @@ HKV_DEV bool grid_sync(unsigned int* bar, unsigned int& sense, uint32_t* lds_fla
       __threadfence();
       __hip_atomic_store(&bar[1], sense, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
+      // (a.force_fault: the test hook that takes the timeout branch at once)
+      const uint32_t limit = a.force_fault ? 0u : (1u << 24);
       uint32_t spins = 0;
       while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sense) {
-        __builtin_amdgcn_s_sleep(8);
-        if (++spins > (1u << 24)) {
+        if (spins++ >= limit) {
           ok = false;
-          atomicExch(&bar[2], 1u);
+          atomicOr(a.fault, 1u);
+          if (a.status) atomicOr(a.status, (uint32_t)HKV_STATUS_TAIL_FAULT);
           break;
         }
+        __builtin_amdgcn_s_sleep(8);
       }
     }
     __threadfence();
@@ -2486,29 +2499,44 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t buf[16 * PAIR_TPB];  // sha256_stream blocks ([word][thread])
   __shared__ uint32_t okf;
+  // this launch's barrier slot [arrivals, sense] (zeroed by the launch before
+  // it on the device's ordered stream of calls); the other slot is the next
+  // launch's, and nothing of this launch touches it
+  unsigned int* bar = a.bar + (a.epoch & 1u) * 4u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned int* nx = a.bar + ((a.epoch + 1u) & 1u) * 4u;
+    __hip_atomic_store(&nx[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&nx[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // the scan's running sum (final: the scan ran before this launch on the
   // stream); every workgroup reads it before its first grid barrier, and
   // workgroup 0 re-arms it after that barrier (or on a barrier fault)
   const unsigned long long total = __hip_atomic_load(a.total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
   if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid, nothing to re-arm
-  unsigned int sense = __hip_atomic_load(&a.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned int sense = 0;   // (the slot starts at [0, 0])
   auto rearm = [&]() {
     if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   const uint32_t tid = blockIdx.x * PAIR_TPB + threadIdx.x, nthr = gridDim.x * PAIR_TPB;
-  // 1. the BIP143 per-tx hashes (lanes: hash-major, so a wave mostly shares its hash)
+  // 1. the BIP143 per-tx hashes (lanes: hash-major, so a wave mostly shares
+  //    its hash). Every tx of the batch is hashed, and the block kernel built
+  //    index rows only for the txs its inputs reference (a block's coinbase
+  //    has none), so each lane re-derives its tx's row from the offsets — a
+  //    stale row of an earlier call would point the hash outside the tx — and
+  //    writes back only the hash words.
   if (a.hash_txs != TX_HASHES_NONE && a.n_tx) {
     const uint32_t items = 3 * a.n_tx;
     for (uint32_t b = 0; b < items; b += nthr) {
       const uint32_t it = b + tid;
       bool go = it < items;
       const uint32_t t = go ? it % a.n_tx : 0, which = go ? it / a.n_tx : 0;
-      uint32_t* row = a.txt + (size_t)t * TXT_WORDS;
+      uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (go) tx_index_row(a.txs, a.tx_off, t, row);
       if (go && a.hash_txs == TX_HASHES_WITNESS) go = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
-      tx_hash_word_lane(a.txs, row, which, go, buf);
+      tx_hash_word_lane(a.txs, row, a.txt + (size_t)t * TXT_WORDS, which, go, buf);
     }
-    if (!grid_sync(a.bar, sense, &okf)) return rearm();
+    if (!grid_sync(a, bar, sense, &okf)) return rearm();
   }
   // 2. key-check and candidate records
   for (uint32_t b = 0; b < a.n; b += nthr) {
@@ -2516,7 +2544,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
     ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
                  a.cand, a.keyrec, buf);
   }
-  if (!grid_sync(a.bar, sense, &okf)) return rearm();
+  if (!grid_sync(a, bar, sense, &okf)) return rearm();
   rearm();  // (every workgroup has read the total)
   // 3. key checks, then the candidates in pair-form groups of 32
   for (uint32_t b = 0; b < n_keys; b += nthr)
@@ -2530,7 +2558,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
                       reinterpret_cast<uint32_t*>(a.cand) + (size_t)shift * REC_WORDS, HKV_MODE_HASKOIN, nullptr,
                       none, qlds, hlds, xch, buf);
   }
-  if (!grid_sync(a.bar, sense, &okf)) return rearm();
+  if (!grid_sync(a, bar, sense, &okf)) return rearm();
   // 4. the countMulSig walk
   for (uint32_t b = 0; b < a.n; b += nthr) {
     const uint32_t jx = b + tid;
@@ -2616,8 +2644,15 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
 }
 uint32_t ms_tail_slots(uint32_t n_cu) { return n_cu * PAIR_SIGS; }
 hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st) {
+#if HKV_TAIL_COOP
+  MsTail arg = a;
+  void* params[] = {&arg};
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&hkv_ms_tail_kernel), dim3(n_cu), dim3(PAIR_TPB),
+                                    params, 0, st);
+#else
   hipLaunchKernelGGL(hkv_ms_tail_kernel, dim3(n_cu), dim3(PAIR_TPB), 0, st, a);
   return hipGetLastError();
+#endif
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
   hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div((size_t)GTAB_TABLES * GTAB_ENTRIES, WG)), dim3(WG), 0, st,

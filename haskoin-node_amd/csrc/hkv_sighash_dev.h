@@ -1509,17 +1509,13 @@ HKV_DEV void ms_resolve_lane(const uint32_t* __restrict__ desc, const uint64_t* 
 }
 
 // One BIP143 per-tx hash (which: 0 hashPrevouts, 1 hashSequence, 2
-// hashOutputs) of a tx whose index row is already built, into its row (the
-// tail kernel's first phase on the fused block path, whose index pass hashed
-// nothing). Block-synchronous like ms_emit_lane.
-HKV_DEV void tx_hash_word_lane(const uint8_t* __restrict__ txs, uint32_t* __restrict__ row_out, uint32_t which,
-                               bool go, uint32_t* buf) {
-  uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (go) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) row[k] = row_out[k];
-    go = (row[TXT_FLAGS] & TXF_OK) != 0;
-  }
+// hashOutputs) of a tx whose index row the caller has built (row), into its
+// row in txt (row_out: only the hash words are written) — the tail kernel's
+// first phase on the fused block path, whose index pass hashed nothing.
+// Block-synchronous like ms_emit_lane.
+HKV_DEV void tx_hash_word_lane(const uint8_t* __restrict__ txs, const uint32_t row[8], uint32_t* __restrict__ row_out,
+                               uint32_t which, bool go, uint32_t* buf) {
+  go = go && (row[TXT_FLAGS] & TXF_OK) != 0;
   Gen g;
   uint32_t h[8], d[8];
   gen_clear(g);

@@ -20,6 +20,8 @@ HKV_HDR_POW_OK, HKV_HDR_LINK_OK, HKV_HDR_NEGATIVE, HKV_HDR_OVERFLOW = 0x01, 0x02
 HKV_HDR_ZERO_TARGET, HKV_HDR_ABOVE_LIMIT, HKV_HDR_HASH_ABOVE = 0x10, 0x20, 0x40
 
 HKV_OK = 0
+HKV_FAIL_NONE, HKV_FAIL_ENQUEUE, HKV_FAIL_JOIN, HKV_FAIL_ALLOC, HKV_FAIL_TAIL = 0, 1, 2, 3, 4
+HKV_STATUS_TAIL_FAULT = 1
 _ERRS = {-1: "HKV_E_ARG", -2: "HKV_E_NODEV", -3: "HKV_E_OOM", -4: "HKV_E_HIP", -5: "HKV_E_INTERNAL"}
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -87,6 +89,9 @@ EXPORTS = {
                                       c_void_p, c_void_p]),
     "hkv_verify_std_inputs_device": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
                                              c_void_p, c_void_p, c_void_p]),
+    "hkv_verify_std_inputs_device_status": (c_int, [c_void_p, c_int, POINTER(HkvTxs), c_void_p, c_size_t,
+                                                    ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hkv_device_fault": (c_int, [c_void_p, c_int, POINTER(c_uint32)]),
     "hkv_verify_std_inputs": (c_int, [c_void_p, POINTER(HkvTxs), c_void_p, c_size_t, ctypes.c_int32,
                                       POINTER(c_uint32)]),
     "hkv_merkle_roots": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),

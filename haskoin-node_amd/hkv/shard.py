@@ -51,16 +51,23 @@ class ShardedVerify:
     verify: called as verify(lo, hi, bits) — must write the verdict words of
     records [lo, hi) into the int32 tensor ``bits`` (hkv_verify_device on the
     rank's GPU in bench.py; a CPU checker in the gloo tests).
-    dist: torch.distributed (None or world == 1: no collective)."""
+    dist: torch.distributed (None or world == 1: no collective).
+    gather_on_host: the all-gather runs on host copies of the words (a gloo
+    group: bench.py --share-device, every rank on one GPU, which RCCL does
+    not allow)."""
 
-    def __init__(self, torch, n: int, rank: int, world: int, verify: Callable, dist=None, device: str = "cuda"):
+    def __init__(self, torch, n: int, rank: int, world: int, verify: Callable, dist=None, device: str = "cuda",
+                 gather_on_host: bool = False):
         self.n, self.rank, self.world = n, rank, world
         self.lo, self.hi = shard_bounds(n, rank, world)
         self.wpr = words_per_rank(n, world)
         self.verify = verify
         self.dist = dist if world > 1 else None
         self.bits = torch.zeros(self.wpr, dtype=torch.int32, device=device)
-        self.gathered = torch.zeros(self.wpr * world, dtype=torch.int32, device=device) if self.dist else None
+        gdev = "cpu" if gather_on_host else device
+        self.host_bits = torch.zeros(self.wpr, dtype=torch.int32, device="cpu") \
+            if gather_on_host and self.dist else None
+        self.gathered = torch.zeros(self.wpr * world, dtype=torch.int32, device=gdev) if self.dist else None
 
     @property
     def local_n(self) -> int:
@@ -70,7 +77,11 @@ class ShardedVerify:
         """Verify the shard, then the one all-gather of the verdict words."""
         self.verify(self.lo, self.hi, self.bits)
         if self.dist is not None:
-            self.dist.all_gather_into_tensor(self.gathered, self.bits)
+            if self.host_bits is not None:
+                self.host_bits.copy_(self.bits)  # (synchronous D2H: after the verify on the current stream)
+                self.dist.all_gather_into_tensor(self.gathered, self.host_bits)
+            else:
+                self.dist.all_gather_into_tensor(self.gathered, self.bits)
 
     def bitmap(self) -> np.ndarray:
         """The global verdict bitmap (ceil(n/32) words) after step()."""

@@ -127,11 +127,25 @@ class Verifier:
         check(rc, "hkv_std_inputs_device", self.lib)
 
     def verify_std_inputs_device(self, dev: int, d_txs, d_jobs: int, n: int, forkid: int, d_records: int,
-                                 d_bits: int, stream_ptr: int = 0) -> None:
+                                 d_bits: int, stream_ptr: int = 0, d_status: int = 0) -> None:
+        """hkv_verify_std_inputs_device, or with d_status (a device word the
+        caller zeroed) hkv_verify_std_inputs_device_status."""
+        if d_status:
+            rc = self.lib.hkv_verify_std_inputs_device_status(
+                self.ctx, dev, ctypes.byref(d_txs), ctypes.c_void_p(d_jobs), n, forkid, ctypes.c_void_p(d_records),
+                ctypes.c_void_p(d_bits), ctypes.c_void_p(d_status), ctypes.c_void_p(stream_ptr or None))
+            check(rc, "hkv_verify_std_inputs_device_status", self.lib)
+            return
         rc = self.lib.hkv_verify_std_inputs_device(self.ctx, dev, ctypes.byref(d_txs), ctypes.c_void_p(d_jobs), n,
                                                    forkid, ctypes.c_void_p(d_records), ctypes.c_void_p(d_bits),
                                                    ctypes.c_void_p(stream_ptr or None))
         check(rc, "hkv_verify_std_inputs_device", self.lib)
+
+    def device_fault(self, dev: int) -> int:
+        """hkv_device_fault: read and clear device dev's sticky fault latch."""
+        w = ctypes.c_uint32(0)
+        check(self.lib.hkv_device_fault(self.ctx, dev, ctypes.byref(w)), "hkv_device_fault", self.lib)
+        return w.value
 
     def gen_keys_device(self, dev: int, seed: int, n: int, d_priv: int, d_pub: int, d_h160: int,
                         stream_ptr: int = 0) -> None:

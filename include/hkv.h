@@ -115,6 +115,10 @@ int hkv_device_failures(hkv_ctx* ctx, int dev);
 #define HKV_FAIL_ENQUEUE 1u
 #define HKV_FAIL_JOIN 2u
 #define HKV_FAIL_ALLOC 3u
+/* HKV_FAIL_TAIL: the next multisig tail launch on device k takes its grid
+ * barrier's timeout branch at once (as if its workgroups were not
+ * co-resident), so the fault reporting below can be tested. */
+#define HKV_FAIL_TAIL 4u
 int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when);
 
 /* Pinned host record buffer with room for max_n records. */
@@ -249,12 +253,34 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * gated on events recorded after the call. Batches run in chunks of 131,072
  * inputs (the multisig scratch is sized per chunk by its 16-of-16 bound, 136
  * candidate + 16 key-check records per input, allocated on first use).
+ * Scratch footprint: (136 + 16) * 168 B per input of the largest chunk seen,
+ * i.e. ~0.1 GB for a 4,000-input block, ~3.35 GB for a full 131,072 chunk.
+ * A multisig tail whose grid barrier gave up leaves its multisig verdicts
+ * at 0 and reports HKV_STATUS_TAIL_FAULT (below) — this form only through
+ * hkv_device_fault; use the _status form to get it per call.
  * n <= 0xFFFFFF00. */
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                                  int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream);
+/* Status bits a verify call reports (hkv_verify_std_inputs_device_status,
+ * hkv_device_fault). HKV_STATUS_TAIL_FAULT: the multisig tail's grid barrier
+ * gave up waiting (its workgroups were not co-resident — the tail is launched
+ * cooperatively, so this should not happen): some multisig inputs of the
+ * batch were left rejected whatever their signatures. Never a false accept. */
+#define HKV_STATUS_TAIL_FAULT 1u
+/* hkv_verify_std_inputs_device with a status word: d_status (device memory
+ * of `dev`, or NULL) gets the call's HKV_STATUS_* bits ORed in on hip_stream,
+ * so an asynchronous caller learns of a fault when it reads its verdicts.
+ * The caller zeroes it. */
+int hkv_verify_std_inputs_device_status(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs,
+                                        size_t n, int32_t forkid, void* d_records, uint32_t* d_bits,
+                                        uint32_t* d_status, void* hip_stream);
+/* Read and clear device dev's sticky fault latch: HKV_STATUS_* bits of every
+ * verify call on the device since the last read (any entry point). Waits for
+ * the device's enqueued calls. */
+int hkv_device_fault(hkv_ctx* ctx, int dev, uint32_t* fault);
 /* Host-memory form of the above; writes ceil(n/32) verdict words. Blocking.
- * Same bound on n. HKV_E_INTERNAL if the multisig tail's grid barrier gave up
- * (its workgroups were not co-resident: the multisig verdicts stayed 0). */
+ * Same bound on n. HKV_E_INTERNAL if this call's multisig tail reported
+ * HKV_STATUS_TAIL_FAULT (some multisig verdicts stayed 0). */
 int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job* jobs, size_t n, int32_t forkid,
                           uint32_t* verdict_bits);
 

@@ -406,9 +406,10 @@ def _ms_oracle(coracle, txs, jobs, forkid):
     return multisig_verdicts(coracle, [sh.tx_parse(t) for t in txs], jobs, forkid)
 
 
-def _device_verify_std(torch, ver, raw_txs, inputs, forkid, records=False):
+def _device_verify_std(torch, ver, raw_txs, inputs, forkid, records=False, status=False):
     """hkv_verify_std_inputs_device over HBM-resident txs / jobs (records:
-    also the 168-byte records the call wrote)."""
+    also the 168-byte records the call wrote; status: through
+    hkv_verify_std_inputs_device_status, also the call's status word)."""
     import hkv
     from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
     tb = TxBatch(raw_txs)
@@ -422,11 +423,14 @@ def _device_verify_std(torch, ver, raw_txs, inputs, forkid, records=False):
     dt = hkv.HkvTxs(d_bytes.data_ptr(), d_off.data_ptr(), len(raw_txs), d_pool.data_ptr(), tb._len)
     recs = torch.zeros(len(inputs) * 168, dtype=torch.uint8, device="cuda")
     bits = torch.zeros(((len(inputs) + 63) // 64) * 2, dtype=torch.int32, device="cuda")
+    st = torch.zeros(2, dtype=torch.int32, device="cuda")
     ver.verify_std_inputs_device(0, dt, d_jobs.data_ptr(), len(inputs), -1 if forkid is None else forkid,
-                                 recs.data_ptr(), bits.data_ptr())
+                                 recs.data_ptr(), bits.data_ptr(), d_status=st.data_ptr() if status else 0)
     torch.cuda.synchronize()
     w = bits.cpu().numpy().view(np.uint32)
     got = [bool((w[k // 32] >> (k % 32)) & 1) for k in range(len(inputs))]
+    if status:
+        return got, int(st[0].item())
     return (got, recs.cpu().numpy().tobytes()) if records else got
 
 
@@ -656,3 +660,252 @@ def test_std_inputs_device_returns_before_the_stream_runs(torch, ver, coracle):
     got = [bool((w[k // 32] >> (k % 32)) & 1) for k in range(len(jobs))]
     assert got == want
     assert int(bbits[: n_big // 32].cpu().numpy().view(np.uint32).astype(np.uint64).sum()) == (n_big // 32) * 0xFFFFFFFF
+
+
+def _ms_block(rng, forkid, n_single=40):
+    """A block-kernel-sized batch: tx 0 a coinbase no input spends (no job
+    references it, so the block kernel builds no index row for it), signed
+    single-signature txs and the multisig cases, shuffled."""
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(24)]
+    mtxs, mjobs, names = txgen.multisig_cases(rng, keys, forkid)
+    btxs, bjobs = txgen.std_block(rng, n_single, keys, forkid=forkid, p2wpkh_share=0.4, p2pk_share=0.2,
+                                  p2sh_share=0.2)
+    cb = sh.Tx(1, [sh.TxIn(b"\0" * 32 + b"\xff" * 4, 0, b"\x03\x01\x02\x03", 0xFFFFFFFF)],
+               [sh.TxOut(50 * 10**8, sh.p2wpkh_script(b"\x11" * 20))], [[b"\0" * 32]], 0)
+    raw = [sh.tx_serialize(cb)] + [sh.tx_serialize(t) for t in btxs + mtxs]
+    jobs = [(t + 1, i, p, v) for (t, i, p, v) in bjobs] + [(t + 1 + len(btxs), i, p, v) for (t, i, p, v) in mjobs]
+    labels = ["single"] * len(bjobs) + names
+    order = list(range(len(jobs)))
+    rng.shuffle(order)
+    return raw, [jobs[k] for k in order], [labels[k] for k in order]
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_tail_hashes_txs_no_input_references(torch, ver, coracle, forkid):
+    """the multisig tail hashes every tx of the batch
+    (BIP143 per-tx hashes), but the block kernel builds index rows only for
+    the txs its inputs reference — a block's coinbase has none. The rows
+    are left over from an earlier call over a much larger tx buffer (a
+    sighash batch of large witness txs, so the stale rows carry TXF_OK |
+    TXF_WITNESS and offsets far past this batch's buffer). The tail now
+    re-derives each row from the offsets: verdicts equal the oracle's
+    through both entry points, and again after a second stale fill."""
+    import hkv
+    rng = random.Random(9090 + (forkid or 0))
+    raw, jobs, labels = _ms_block(rng, forkid)
+    assert len(jobs) <= 16 * 256 and all(t != 0 for (t, _, _, _) in jobs)
+    want = _ms_oracle(coracle, raw, jobs, forkid)
+    big = [sh.tx_serialize(txgen.rand_tx(rng, 40, 30, segwit=True)) for _ in range(len(raw) + 8)]
+    for rep in range(2):
+        sj = [(t, 0, b"\x51", 1, 1, 1) for t in range(len(big))]
+        hkv.tx_sig_hash_batch(ver, big, sj, forkid)  # fills the txt rows of every tx index of this batch
+        got = _device_verify_std(torch, ver, raw, jobs, forkid)
+        bad = [(labels[k], got[k], want[k]) for k in range(len(jobs)) if got[k] != want[k]]
+        assert not bad, bad[:10]
+        hkv.tx_sig_hash_batch(ver, big, sj, forkid)
+        assert hkv.verify_std_inputs(ver, raw, jobs, forkid) == want
+    assert sum(g for g, lb in zip(want, labels) if lb != "single") > 40
+
+
+def test_tail_barrier_fault_reported_then_clean(torch, ver, coracle):
+    """VERDICT r04 item 3 / ADVICE r04: a multisig tail whose grid barrier
+    gives up (forced by the HKV_FAIL_TAIL hook) reports the fault through
+    the device form's status word, the device's sticky latch
+    (hkv_device_fault, read-and-clear) and the host form's return code
+    (HKV_E_INTERNAL); its multisig verdicts are rejects only (never an
+    accept the oracle does not give), the single-signature verdicts are
+    untouched, and the next call — whose barrier uses the other slot,
+    which the faulted launch zeroed — is bit-exact again with no fault."""
+    import hkv
+    from hkv.lib import HKV_FAIL_TAIL, HKV_STATUS_TAIL_FAULT, HkvError
+    rng = random.Random(5151)
+    raw, jobs, labels = _ms_block(rng, None)
+    want = _ms_oracle(coracle, raw, jobs, None)
+    assert ver.device_fault(0) == 0
+    # the device form with a status word
+    assert ver.lib.hkv_debug_fail_device(ver.ctx, 0, HKV_FAIL_TAIL) == 0
+    got, st = _device_verify_std(torch, ver, raw, jobs, None, status=True)
+    assert st == HKV_STATUS_TAIL_FAULT
+    assert all(w or not g for g, w in zip(got, want))            # no false accept
+    assert all(g == w for g, w, lb in zip(got, want, labels) if lb == "single")
+    assert any(w and not g for g, w in zip(got, want))           # the fault cost some multisig accepts
+    assert ver.device_fault(0) == HKV_STATUS_TAIL_FAULT
+    assert ver.device_fault(0) == 0                              # read-and-clear
+    got, st = _device_verify_std(torch, ver, raw, jobs, None, status=True)
+    assert st == 0 and got == want
+    # the plain device form: the latch only
+    assert ver.lib.hkv_debug_fail_device(ver.ctx, 0, HKV_FAIL_TAIL) == 0
+    got = _device_verify_std(torch, ver, raw, jobs, None)
+    assert all(w or not g for g, w in zip(got, want))
+    assert ver.device_fault(0) == HKV_STATUS_TAIL_FAULT
+    # the host form: its own call's status
+    assert ver.lib.hkv_debug_fail_device(ver.ctx, 0, HKV_FAIL_TAIL) == 0
+    with pytest.raises(HkvError) as ei:
+        hkv.verify_std_inputs(ver, raw, jobs)
+    assert ei.value.rc == -5
+    assert hkv.verify_std_inputs(ver, raw, jobs) == want         # an earlier fault is not this call's
+    assert _device_verify_std(torch, ver, raw, jobs, None) == want
+    assert ver.device_fault(0) == HKV_STATUS_TAIL_FAULT          # (the host-form fault above)
+    assert ver.device_fault(0) == 0
+
+
+# --- malformed wire data on the block kernel's LDS tx view ----------------------
+
+def _segments(tx):
+    """The wire form of tx as named segments (so a test can rewrite one
+    field — a count, a length varint — and keep the rest byte-exact)."""
+    seg = any(len(w) for w in tx.witness)
+    out = [("ver", tx.version.to_bytes(4, "little"))]
+    if seg:
+        out.append(("marker", b"\x00\x01"))
+    out.append(("nin", sh.put_varint(len(tx.inputs))))
+    for j, ti in enumerate(tx.inputs):
+        out += [(f"in{j}_op", ti.outpoint()), (f"in{j}_sl", sh.put_varint(len(ti.script))), (f"in{j}_s", ti.script),
+                (f"in{j}_seq", ti.sequence.to_bytes(4, "little"))]
+    out.append(("nout", sh.put_varint(len(tx.outputs))))
+    for k, to in enumerate(tx.outputs):
+        out += [(f"out{k}_v", to.value.to_bytes(8, "little")), (f"out{k}_sl", sh.put_varint(len(to.script))),
+                (f"out{k}_s", to.script)]
+    if seg:
+        for j, w in enumerate(tx.witness):
+            out.append((f"w{j}_n", sh.put_varint(len(w))))
+            for q, item in enumerate(w):
+                out += [(f"w{j}_{q}_l", sh.put_varint(len(item))), (f"w{j}_{q}", item)]
+    out.append(("lock", tx.locktime.to_bytes(4, "little")))
+    assert b"".join(b for _, b in out) == sh.tx_serialize(tx)
+    return out
+
+
+def _rewrite(tx, name, new):
+    return b"".join(new if n == name else b for n, b in _segments(tx))
+
+
+def _padded(rng, keys, kind, target, forkid=None):
+    """A signed one-job tx of exactly `target` bytes: input 0 spends a
+    `kind` prevout, input 1 is padding whose scriptSig neither sighash form
+    commits to (legacy blanks the other inputs' scripts, BIP143 hashes only
+    their outpoints and sequences), grown after signing to hit the size."""
+    while True:
+        txs, jobs = txgen.std_block(rng, 1, keys, forkid=forkid, nin_choices=(2,),
+                                    p2wpkh_share=1.0 if kind == "p2wpkh" else 0.0)
+        tx = txs[0]
+        if kind == "p2pkh" and len(jobs[0][2]) != 25:
+            continue
+        tx.inputs[1].script = b""
+        base = len(sh.tx_serialize(tx))
+        for pad in range(max(0, target - base - 4), target - base + 1):
+            if base + pad + len(sh.put_varint(pad)) - 1 == target:
+                tx.inputs[1].script = b"\x6a" * pad
+                raw = sh.tx_serialize(tx)
+                assert len(raw) == target
+                return tx, raw, jobs[0]
+
+
+@pytest.mark.parametrize("forkid", [None, 0])
+def test_block_kernel_malformed_wire_vs_oracle(torch, ver, coracle, forkid):
+    """VERDICT r04 item 4 (after the round-4 aperture violation on the block
+    kernel's LDS tx view): at block size, through both standard-input entry
+    points, txs whose wire form lies — truncated at several points, input /
+    output counts and scriptSig / output-script / witness varints (1-, 3-,
+    5- and 9-byte forms) that claim more bytes than the tx holds, a tx of
+    under 10 bytes and an empty one — beside valid txs of exactly 2,047,
+    2,048 (the LDS copy's limit) and 2,049 bytes, a 2,049-byte tx cut to
+    2,048, a prevout script that ends at the script pool's last byte and a
+    job whose script range runs past the pool. Every verdict equals the
+    oracle's (a tx that does not parse rejects), and every record the block
+    kernel wrote equals the oracle's (all-zero for a reject)."""
+    import hkv
+    from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
+    rng = random.Random(2049 + (forkid or 0))
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(8)]
+    txs, jobs = txgen.std_block(rng, 30, keys, forkid=forkid, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
+    raw = [sh.tx_serialize(t) for t in txs]
+    jobs = list(jobs)
+    names = ["valid"] * len(jobs)
+
+    def add(b, job, name):
+        raw.append(b)
+        jobs.append((len(raw) - 1,) + tuple(job[1:]))
+        names.append(name)
+
+    # the signed txs the mutations start from: every template of std_block
+    bases = [(txs[t], (t, i, p, v)) for (t, i, p, v) in jobs[:12]]
+    big = [b"\xfd\xff\xff", b"\xfe\xff\xff\xff\xff", b"\xff" + b"\xff" * 8, b"\xfe\x00\x00\x01\x00"]
+    for bt, job in bases:
+        b = sh.tx_serialize(bt)
+        for cut in (1, 4, 5, len(b) // 2, len(b) - 9):
+            add(b[:-cut], job, f"trunc{cut}")
+        i = job[1]
+        segs = dict(_segments(bt))
+        add(_rewrite(bt, "nin", sh.put_varint(len(bt.inputs) + 1)), job, "nin+1")
+        add(_rewrite(bt, "nout", sh.put_varint(len(bt.outputs) + 1)), job, "nout+1")
+        add(_rewrite(bt, f"in{i}_sl", sh.put_varint(len(bt.inputs[i].script) + 1)), job, "sl+1")
+        add(_rewrite(bt, "out1_sl", sh.put_varint(len(bt.outputs[1].script) + 5)), job, "osl+5")
+        for v in big:
+            add(_rewrite(bt, "nin", v), job, "nin_big")
+            add(_rewrite(bt, "nout", v), job, "nout_big")
+            add(_rewrite(bt, f"in{i}_sl", v), job, "sl_big")
+            add(_rewrite(bt, "out0_sl", v), job, "osl_big")
+        if f"w{i}_n" in segs:
+            for v in big[:2]:
+                add(_rewrite(bt, f"w{i}_n", v), job, "wn_big")
+                add(_rewrite(bt, f"w{i}_0_l", v), job, "wl_big")
+            add(_rewrite(bt, f"w{i}_n", sh.put_varint(len(bt.witness[i]) + 1)), job, "wn+1")
+    add(b"\x01\x00\x00\x00\x01\x00", bases[0][1], "short")
+    add(b"", bases[0][1], "empty")
+    for kind in ("p2pkh", "p2wpkh"):
+        for size in (2047, 2048, 2049):
+            _, b, job = _padded(rng, keys, kind, size, forkid)
+            add(b, (None,) + tuple(job[1:]), f"{kind}_{size}")
+        _, b, job = _padded(rng, keys, kind, 2049, forkid)
+        add(b[:2048], (None,) + tuple(job[1:]), f"{kind}_2049_cut")
+    # the last job's prevout script is new, so it ends the pool
+    kz = txgen.Key(rng.randrange(1, o.N))
+    ztx, zjobs = txgen.std_block(rng, 1, [kz], forkid=forkid, nin_choices=(1,), p2wpkh_share=0.0)
+    add(sh.tx_serialize(ztx[0]), (None,) + tuple(zjobs[0][1:]), "pool_end")
+    assert len(jobs) <= 16 * 256
+
+    parsed = []
+    for b in raw:
+        try:
+            parsed.append(sh.tx_parse(b))
+        except (ValueError, IndexError):
+            parsed.append(None)
+    exp = [sh.std_input_record(parsed[t], i, p, v, forkid) if parsed[t] is not None else b"\0" * 168
+           for (t, i, p, v) in jobs]
+    want = oracle_batch(coracle, b"".join(exp), 1).tolist()
+    for n, w in zip(names, want):
+        if n == "valid" or n[-4:] in ("2047", "2048", "2049") or n == "pool_end":
+            assert w, n
+    assert sum(not w for w in want) > 100
+
+    def check(got, recs=None):
+        bad = [(names[k], got[k], want[k]) for k in range(len(jobs)) if got[k] != want[k]]
+        assert not bad, bad[:10]
+        if recs is not None:
+            badr = [names[k] for k in range(len(jobs)) if recs[k * 168:(k + 1) * 168] != exp[k]]
+            assert not badr, badr[:10]
+
+    check(hkv.verify_std_inputs(ver, raw, jobs, forkid))
+    check(*_device_verify_std(torch, ver, raw, jobs, forkid, records=True))
+    # the pool-end job: its script is the pool's last bytes; a job whose range
+    # runs past the pool (or wraps) rejects
+    tb = TxBatch(raw)
+    arr = np.zeros(len(jobs) + 2, dtype=INPUT_JOB_DTYPE)
+    for k, (t, i, spk, value) in enumerate(jobs):
+        off, ln = tb.script(spk)
+        arr[k] = (t, i, off, ln, value)
+    assert arr[len(jobs) - 1]["script_off"] + arr[len(jobs) - 1]["script_len"] == tb._len
+    last = arr[len(jobs) - 1]
+    arr[len(jobs)] = (last["tx"], last["input"], last["script_off"] + 1, last["script_len"], last["value"])
+    arr[len(jobs) + 1] = (last["tx"], last["input"], 0xFFFFFFF0, 0x20, last["value"])
+    st, pool = tb.struct()
+    words = np.zeros((len(arr) + 31) // 32, dtype=np.uint32)
+    rc = ver.lib.hkv_verify_std_inputs(ver.ctx, ctypes.byref(st), arr.ctypes.data, len(arr),
+                                       -1 if forkid is None else forkid,
+                                       words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    assert rc == 0
+    from hkv.records import unpack_bits
+    got = unpack_bits(words, len(arr)).tolist()
+    check(got[:len(jobs)])
+    assert got[len(jobs):] == [False, False]
