@@ -670,7 +670,7 @@ def _ms_block(rng, forkid, n_single=40):
     mtxs, mjobs, names = txgen.multisig_cases(rng, keys, forkid)
     btxs, bjobs = txgen.std_block(rng, n_single, keys, forkid=forkid, p2wpkh_share=0.4, p2pk_share=0.2,
                                   p2sh_share=0.2)
-    cb = sh.Tx(1, [sh.TxIn(b"\0" * 32 + b"\xff" * 4, 0, b"\x03\x01\x02\x03", 0xFFFFFFFF)],
+    cb = sh.Tx(1, [sh.TxIn(b"\0" * 32, 0xFFFFFFFF, b"\x03\x01\x02\x03", 0xFFFFFFFF)],
                [sh.TxOut(50 * 10**8, sh.p2wpkh_script(b"\x11" * 20))], [[b"\0" * 32]], 0)
     raw = [sh.tx_serialize(cb)] + [sh.tx_serialize(t) for t in btxs + mtxs]
     jobs = [(t + 1, i, p, v) for (t, i, p, v) in bjobs] + [(t + 1 + len(btxs), i, p, v) for (t, i, p, v) in mjobs]
