@@ -1047,7 +1047,9 @@ def main() -> None:
             workload = (f"BASELINE configs[4]: one IBD-style batch of {n_total:,} records (configs[1] distribution "
                         f"plus {inv / 10:g}% invalid: flipped msg32 / r / s bit, another key, the negated key; "
                         f"seed 0x{seed:X}), contiguous 64-aligned shards, each rank generating only its slice; "
-                        f"one RCCL all-gather of the verdict bitmap per step")
+                        + ("one gloo all-gather of the verdict words through host memory per step (--share-device: "
+                           "every rank on device 0; a test of the N > 1 code path, not a scaling point)" if share else
+                           "one RCCL all-gather of the verdict bitmap per step"))
         else:
             workload = ("BASELINE configs[1]: 1,048,576 valid (hash,r,s,pubkey) per GPU, 90% compressed / 10% "
                         "uncompressed keys, 65,536-key pool")

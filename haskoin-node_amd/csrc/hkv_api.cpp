@@ -72,10 +72,10 @@ struct DevCtx {
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   void* ms_ctr = nullptr;            // scan counters: [0] running sum (the tail reads and re-arms it)
-  // the tail kernel's words: [0..3] and [4..7] the two grid-barrier slots
-  // (arrivals, sense; launch `tail_epoch` uses slot tail_epoch & 1 and zeroes
-  // the other), [8] the sticky fault latch (hkv_device_fault), [9] the host
-  // form's per-call status word
+  // the tail kernel's words: [0..7] and [8..15] the two work-queue slots
+  // (claim, done per phase; launch `tail_epoch` uses slot tail_epoch & 1 and
+  // zeroes the other), [16] the sticky fault latch (hkv_device_fault), [17]
+  // the host form's per-call status word
   unsigned int* ms_bar = nullptr;
   uint32_t tail_epoch = 0;
   bool inject_tail = false;          // hkv_debug_fail_device(HKV_FAIL_TAIL): the next tail launch's barriers give up
@@ -153,7 +153,7 @@ size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 constexpr size_t STD_CHUNK = 1u << 17;
 constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
 constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFF00ull;
-constexpr size_t MS_BAR_WORDS = 16, MS_FAULT = 8, MS_HOST_STATUS = 9;  // DevCtx::ms_bar
+constexpr size_t MS_BAR_WORDS = 32, MS_FAULT = 16, MS_HOST_STATUS = 17;  // DevCtx::ms_bar
 
 int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
   if (d.im_cap < n_pad) {

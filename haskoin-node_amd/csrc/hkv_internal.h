@@ -68,11 +68,11 @@ struct MsTail {
   const uint32_t* gtab;
   uint32_t* qs;
   uint32_t* out_bits;               // the batch's verdict words (multisig inputs are ORed in)
-  unsigned int* bar;                // two grid-barrier slots [arrivals, sense, -, -]: launch `epoch` uses slot epoch & 1
+  unsigned int* bar;                // two work-queue slots of 8 words (claim, done[4]): launch `epoch` uses slot epoch & 1
   uint32_t epoch;                   // this launch's sequence number on the device
   unsigned int* fault;              // the device's sticky fault latch (hkv_device_fault)
   uint32_t* status;                 // the call's status word (HKV_STATUS_* ORed in), or null
-  uint32_t force_fault;             // test hook (hkv_debug_fail_device HKV_FAIL_TAIL): every barrier wait gives up
+  uint32_t force_fault;             // test hook (hkv_debug_fail_device HKV_FAIL_TAIL): every phase wait gives up
 };
 hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st);
 uint32_t ms_tail_slots(uint32_t n_cu);  // signatures in flight (im / aux slots the tail needs)

@@ -2447,50 +2447,37 @@ namespace hkv {
 //          on slot-relative scratch sized by the grid;
 //       4. per input, haskoin's countMulSig over its candidate verdicts
 //          (ms_resolve_lane), ORed into the batch's verdict words.
-//     The grid is one workgroup per CU, launched cooperatively (HKV_TAIL_COOP:
-//     hipLaunchCooperativeKernel fails rather than start a grid whose
-//     workgroups cannot all be resident), so the barriers cannot starve.
-//     Their spin is bounded anyway: a workgroup that waits ~seconds gives up,
-//     the multisig verdicts it owns stay 0 (reject, never a false accept: a
-//     barrier releases only when every workgroup has arrived, i.e. has
-//     finished the phase before it), and the fault is reported through the
-//     device's sticky latch and the call's status word (HKV_STATUS_TAIL_FAULT).
-//     Each launch uses its own barrier slot (the epoch's parity) and zeroes
-//     the other one for the next launch, so a faulted launch's leftover
-//     arrivals can never release a later launch's barrier early.
+//     The phases run as one ordered work queue, not as grid barriers: the
+//     launch's items (phase 1's hash chunks, then phase 2's record chunks,
+//     then phase 3's key-check chunks and candidate groups, then phase 4's
+//     walk chunks) are claimed in that order by a device counter, and a
+//     workgroup starts an item only once every item of the phase before has
+//     completed. A workgroup waits only when no earlier item is left to
+//     claim, i.e. for items other workgroups are running — so progress never
+//     depends on a workgroup that is not resident, and the launch needs no
+//     co-residency (a cooperative launch, which guarantees it, cost ~23 us
+//     per call on the block path: profiles/r05a/coop_ab.txt). The wait is
+//     bounded anyway (~seconds, far above one item): a workgroup that gives
+//     up leaves the verdicts it owns at 0 (reject, never a false accept) and
+//     reports HKV_STATUS_TAIL_FAULT through the device's sticky latch and the
+//     call's status word. Each launch counts in its own slot (the epoch's
+//     parity) and zeroes the other for the next launch, so nothing a faulted
+//     launch leaves behind reaches a later one.
 // ---------------------------------------------------------------------------
-#ifndef HKV_TAIL_COOP  // the multisig tail by hipLaunchCooperativeKernel (0: a plain launch)
-#define HKV_TAIL_COOP 1
-#endif
-HKV_DEV bool grid_sync(const MsTail& a, unsigned int* bar, unsigned int& sense, uint32_t* lds_flag) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    sense ^= 1u;
-    bool ok = true;
-    __threadfence();
-    if (atomicAdd(&bar[0], 1u) == gridDim.x - 1) {
-      atomicExch(&bar[0], 0u);
-      __threadfence();
-      __hip_atomic_store(&bar[1], sense, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      // (a.force_fault: the test hook that takes the timeout branch at once)
-      const uint32_t limit = a.force_fault ? 0u : (1u << 24);
-      uint32_t spins = 0;
-      while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sense) {
-        if (spins++ >= limit) {
-          ok = false;
-          atomicOr(a.fault, 1u);
-          if (a.status) atomicOr(a.status, (uint32_t)HKV_STATUS_TAIL_FAULT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
+enum : uint32_t { TQ_CLAIM = 0, TQ_DONE = 1, TQ_SLOT = 8 };  // slot words: claim, done[4]
+// wait (thread 0) until `done` reaches `want`; false on a timeout (fault reported)
+HKV_DEV bool tail_wait(const MsTail& a, unsigned int* done, uint32_t want) {
+  const uint32_t limit = a.force_fault ? 0u : (1u << 24);
+  uint32_t spins = 0;
+  while (__hip_atomic_load(done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    if (spins++ >= limit) {
+      atomicOr(a.fault, 1u);
+      if (a.status) atomicOr(a.status, (uint32_t)HKV_STATUS_TAIL_FAULT);
+      return false;
     }
-    __threadfence();
-    *lds_flag = ok ? 1u : 0u;
+    __builtin_amdgcn_s_sleep(8);
   }
-  __syncthreads();
-  return *lds_flag != 0;
+  return true;
 }
 
 __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
@@ -2498,71 +2485,101 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
   __shared__ HLane hlds[2];
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t buf[16 * PAIR_TPB];  // sha256_stream blocks ([word][thread])
-  __shared__ uint32_t okf;
-  // this launch's barrier slot [arrivals, sense] (zeroed by the launch before
-  // it on the device's ordered stream of calls); the other slot is the next
-  // launch's, and nothing of this launch touches it
-  unsigned int* bar = a.bar + (a.epoch & 1u) * 4u;
+  __shared__ uint32_t item_s, go_s;
+  // this launch's queue slot (zeroed by the launch before it on the device's
+  // ordered stream of calls); the other slot is the next launch's
+  unsigned int* q = a.bar + (a.epoch & 1u) * TQ_SLOT;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    unsigned int* nx = a.bar + ((a.epoch + 1u) & 1u) * 4u;
-    __hip_atomic_store(&nx[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&nx[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned int* nx = a.bar + ((a.epoch + 1u) & 1u) * TQ_SLOT;
+#pragma unroll
+    for (int k = 0; k < (int)TQ_SLOT; ++k) __hip_atomic_store(&nx[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // the scan's running sum (final: the scan ran before this launch on the
-  // stream); every workgroup reads it before its first grid barrier, and
-  // workgroup 0 re-arms it after that barrier (or on a barrier fault)
+  // stream); re-armed by whichever workgroup completes the last item (or gives
+  // up): a workgroup starting after that reads 0 and has nothing to do
   const unsigned long long total = __hip_atomic_load(a.total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
-  if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid, nothing to re-arm
-  unsigned int sense = 0;   // (the slot starts at [0, 0])
-  auto rearm = [&]() {
-    if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  const uint32_t tid = blockIdx.x * PAIR_TPB + threadIdx.x, nthr = gridDim.x * PAIR_TPB;
-  // 1. the BIP143 per-tx hashes (lanes: hash-major, so a wave mostly shares
-  //    its hash). Every tx of the batch is hashed, and the block kernel built
-  //    index rows only for the txs its inputs reference (a block's coinbase
-  //    has none), so each lane re-derives its tx's row from the offsets — a
-  //    stale row of an earlier call would point the hash outside the tx — and
-  //    writes back only the hash words.
-  if (a.hash_txs != TX_HASHES_NONE && a.n_tx) {
-    const uint32_t items = 3 * a.n_tx;
-    for (uint32_t b = 0; b < items; b += nthr) {
-      const uint32_t it = b + tid;
-      bool go = it < items;
-      const uint32_t t = go ? it % a.n_tx : 0, which = go ? it / a.n_tx : 0;
-      uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (go) tx_index_row(a.txs, a.tx_off, t, row);
-      if (go && a.hash_txs == TX_HASHES_WITNESS) go = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
-      tx_hash_word_lane(a.txs, row, a.txt + (size_t)t * TXT_WORDS, which, go, buf);
-    }
-    if (!grid_sync(a, bar, sense, &okf)) return rearm();
-  }
-  // 2. key-check and candidate records
-  for (uint32_t b = 0; b < a.n; b += nthr) {
-    const uint32_t jx = b + tid;
-    ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
-                 a.cand, a.keyrec, buf);
-  }
-  if (!grid_sync(a, bar, sense, &okf)) return rearm();
-  rearm();  // (every workgroup has read the total)
-  // 3. key checks, then the candidates in pair-form groups of 32
-  for (uint32_t b = 0; b < n_keys; b += nthr)
-    key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), b + tid, n_keys, a.kbits);
-  const uint32_t groups = (n_cand + PAIR_SIGS - 1) / PAIR_SIGS, slots = gridDim.x * PAIR_SIGS;
-  const uint32_t sbase = blockIdx.x * PAIR_SIGS;
+  if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid
+  const uint32_t T = PAIR_TPB;
+  const uint32_t n1 = (a.hash_txs != TX_HASHES_NONE) ? (3 * a.n_tx + T - 1) / T : 0;  // hash chunks
+  const uint32_t n2 = (a.n + T - 1) / T;                                                // record chunks
+  const uint32_t n3k = (n_keys + T - 1) / T, n3 = n3k + (n_cand + PAIR_SIGS - 1) / PAIR_SIGS;
+  const uint32_t n4 = n2;                                                               // walk chunks
+  const uint32_t e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4;
+  const uint32_t slots = gridDim.x * PAIR_SIGS, sbase = blockIdx.x * PAIR_SIGS;
   const StdArgs none{};
-  for (uint32_t g = blockIdx.x; g < groups; g += gridDim.x) {
-    const uint32_t base = g * PAIR_SIGS, shift = base - sbase;  // record = slot + shift
-    pair_group<false>(sbase, a.im, n_cand - shift, slots, a.gtab, a.cbits + shift / 32, 0xFFFFFFFFu, a.aux,
-                      reinterpret_cast<uint32_t*>(a.cand) + (size_t)shift * REC_WORDS, HKV_MODE_HASKOIN, nullptr,
-                      none, qlds, hlds, xch, buf);
-  }
-  if (!grid_sync(a, bar, sense, &okf)) return rearm();
-  // 4. the countMulSig walk
-  for (uint32_t b = 0; b < a.n; b += nthr) {
-    const uint32_t jx = b + tid;
-    ms_resolve_lane(a.desc, a.off, jx, jx < a.n, a.cbits, a.kbits, a.out_bits);
+  int seen = 0;  // phases known complete (this workgroup's view)
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint32_t it = atomicAdd(&q[TQ_CLAIM], 1u);
+      const int ph = it < e1 ? 0 : (it < e2 ? 1 : (it < e3 ? 2 : 3));
+      uint32_t ok = it < e4 ? 1u : 0u;
+      // the phase before this item's must be complete (items are claimed in
+      // phase order, so only running items can be outstanding)
+      const uint32_t need[4] = {0u, n1, n2, n3};
+      if (ok && ph > seen) {
+        ok = tail_wait(a, &q[TQ_DONE + ph - 1], need[ph]) ? 1u : 2u;
+        if (ok == 1u) seen = ph;
+      }
+      item_s = it;
+      go_s = ok;
+    }
+    __syncthreads();
+    const uint32_t it = item_s, go = go_s;
+    __syncthreads();
+    if (go != 1u) {
+      if (go == 2u && threadIdx.x == 0)  // gave up: re-arm the scan sum for the next call
+        __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    int ph;
+    if (it < e1) {
+      // 1. the BIP143 per-tx hashes (lanes hash-major, so a wave mostly
+      //    shares its hash). Every tx of the batch is hashed, and the block
+      //    kernel built index rows only for the txs its inputs reference (a
+      //    block's coinbase has none), so each lane re-derives its tx's row
+      //    from the offsets — a stale row of an earlier call would point the
+      //    hash outside the tx — and writes back only the hash words.
+      ph = 0;
+      const uint32_t x = it * T + threadIdx.x;
+      bool go1 = x < 3 * a.n_tx;
+      const uint32_t t = go1 ? x % a.n_tx : 0, which = go1 ? x / a.n_tx : 0;
+      uint32_t row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (go1) tx_index_row(a.txs, a.tx_off, t, row);
+      if (go1 && a.hash_txs == TX_HASHES_WITNESS) go1 = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
+      tx_hash_word_lane(a.txs, row, a.txt + (size_t)t * TXT_WORDS, which, go1, buf);
+    } else if (it < e2) {
+      // 2. key-check and candidate records
+      ph = 1;
+      const uint32_t jx = (it - e1) * T + threadIdx.x;
+      ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
+                   a.cand, a.keyrec, buf);
+    } else if (it < e3) {
+      // 3. a chunk of key checks, or a pair-form group of 32 candidates on
+      //    this workgroup's own scratch slots
+      ph = 2;
+      const uint32_t k = it - e2;
+      if (k < n3k) {
+        key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), k * T + threadIdx.x, n_keys, a.kbits);
+      } else {
+        const uint32_t base = (k - n3k) * PAIR_SIGS, shift = base - sbase;  // record = slot + shift
+        pair_group<false>(sbase, a.im, n_cand - shift, slots, a.gtab, a.cbits + shift / 32, 0xFFFFFFFFu, a.aux,
+                          reinterpret_cast<uint32_t*>(a.cand) + (size_t)shift * REC_WORDS, HKV_MODE_HASKOIN,
+                          nullptr, none, qlds, hlds, xch, buf);
+      }
+    } else {
+      // 4. the countMulSig walk
+      ph = 3;
+      const uint32_t jx = (it - e3) * T + threadIdx.x;
+      ms_resolve_lane(a.desc, a.off, jx, jx < a.n, a.cbits, a.kbits, a.out_bits);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      const uint32_t d = atomicAdd(&q[TQ_DONE + ph], 1u) + 1u;
+      if (ph == 3 && d == n4)  // the launch's last item: re-arm the scan sum
+        __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -2644,15 +2661,8 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
 }
 uint32_t ms_tail_slots(uint32_t n_cu) { return n_cu * PAIR_SIGS; }
 hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st) {
-#if HKV_TAIL_COOP
-  MsTail arg = a;
-  void* params[] = {&arg};
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&hkv_ms_tail_kernel), dim3(n_cu), dim3(PAIR_TPB),
-                                    params, 0, st);
-#else
   hipLaunchKernelGGL(hkv_ms_tail_kernel, dim3(n_cu), dim3(PAIR_TPB), 0, st, a);
   return hipGetLastError();
-#endif
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
   hipLaunchKernelGGL(hkv_gtable_kernel, dim3(ceil_div((size_t)GTAB_TABLES * GTAB_ENTRIES, WG)), dim3(WG), 0, st,

@@ -516,6 +516,32 @@ def reduced_pair_functions():
     return out
 
 
+def row_functions():
+    """Partial products of R rows of a (R limbs) by all 8 limbs of b: the
+    lane-split products (hkv_field.h fe_mul_rows2 / fe_mul_rows4) give each
+    lane of a pair or quad R = 4 or 2 rows of one 256 x 256 product, and
+    the lanes' partials are summed across lanes (DPP) before one reduction."""
+    out = [""]
+    for R in (4, 2):
+        n_out = R + 8
+        out.append(f"// {R} x 8 limb product (rows a[0..{R - 1}] by b[0..7]) -> {n_out} limbs")
+        out.append(f"__device__ __forceinline__ void mul{R}x8_ps(uint32_t t[{n_out}], const uint32_t* a, "
+                   f"const uint32_t* b) {{")
+        out.append("  uint64_t acc = 0;")
+        out.append("  uint32_t top;")
+        out.append("  uint64_t c0, c1, c2;")
+        for k in range(R + 7):
+            pairs = [(i, k - i) for i in range(R) if 0 <= k - i < 8]
+            out.append(f"  // column {k}: {len(pairs)} products")
+            out.append(column_block(k, pairs, "rows"))
+            out.append(f"  t[{k}] = (uint32_t)acc;")
+            out.append("  acc = (acc >> 32) | ((uint64_t)top << 32);")
+        out.append(f"  t[{n_out - 1}] = (uint32_t)acc;")
+        out.append("  (void)c0; (void)c1; (void)c2;")
+        out.append("}")
+    return out
+
+
 def main():
     out = ["// GENERATED by tools/gen_mul_asm.py — do not edit.",
            "// 256x256 -> 512-bit product, product scanning in gfx950 inline asm",
@@ -572,6 +598,7 @@ def main():
     out.append("  }")
     out.append("}")
     out.extend(pair_functions())
+    out.extend(row_functions())
     out.extend(reduced_functions())
     out.extend(reduced_pair_functions())
     out.append("")

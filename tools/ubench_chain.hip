@@ -45,6 +45,82 @@ __device__ __forceinline__ void gej_double_2m5s(gej& r, const gej& a) {
   fe_sub(r.y, t, C);        // Y3' = E'(M - X3') - C
 }
 
+// ---- lane-split products (prototype): the 64 limb
+// products of one 256 x 256 product spread over 2 or 4 lanes of a quad by
+// rows of a, the partials summed across lanes by DPP, one reduction ----
+template <int PERM>
+__device__ __forceinline__ uint32_t dppq(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, PERM, 0xF, 0xF, false);
+}
+constexpr int QP_X2 = 0x4E, QP_X1 = 0xB1, QP_0101 = 0x44, QP_1 = 0x55;  // [2,3,0,1] [1,0,3,2] [0,1,0,1] [1,1,1,1]
+// r = a * b on the lane with hsel = 0 of the pair {q, q ^ 2}; its partner
+// (hsel = all ones) takes a's rows 4..7. Same a, b on both lanes.
+__device__ __forceinline__ void fe_mul_rows2(fe& r, const fe& a, const fe& b, uint32_t hsel) {
+  uint32_t ar[4], p[12], t[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ar[k] = (a.v[k] & ~hsel) | (a.v[k + 4] & hsel);
+  mul4x8_ps(p, ar, b.v);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = p[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[4 + k] = addc(p[4 + k], dppq<QP_X2>(p[k]), c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[12 + k] = addc(0u, dppq<QP_X2>(p[8 + k]), c);
+  fe_reduce512(r, t);
+}
+// r = a * b on quad lane 1: rows 0,1 on lane 1, 2,3 on lane 0, 4,5 on lane
+// 3, 6,7 on lane 2 (m0 / m1 / m2 all ones on quad lane 0 / 1 / 2); same b on
+// every lane
+__device__ __forceinline__ void fe_mul_rows4(fe& r, const fe& a, const fe& b, uint32_t m0, uint32_t m1,
+                                             uint32_t m2) {
+  const uint32_t m3 = ~(m0 | m1 | m2);
+  uint32_t ar[2], p[10], t1[12], t[16];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    ar[k] = (a.v[k] & m1) | (a.v[2 + k] & m0) | (a.v[4 + k] & m3) | (a.v[6 + k] & m2);
+  mul2x8_ps(p, ar, b.v);
+  uint32_t c = 0;
+  t1[0] = p[0];
+  t1[1] = p[1];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t1[2 + k] = addc(p[2 + k], dppq<QP_X1>(p[k]), c);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) t1[10 + k] = addc(0u, dppq<QP_X1>(p[8 + k]), c);
+  c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = t1[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[4 + k] = addc(t1[4 + k], dppq<QP_X2>(t1[k]), c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[12 + k] = addc(0u, dppq<QP_X2>(t1[8 + k]), c);
+  fe_reduce512(r, t);
+}
+// quad_double with the two products that leave lanes idle spread over them:
+// [A | B] as two 2-way row-split squares (X^2 on lanes 0, 2; Y^2 on 1, 3),
+// Y3 = A D - 8C as a 4-way row-split product on lane 1
+__device__ __forceinline__ void quad_double_split(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
+  fe S, R1, Aq, RA, T, opA, opB, R2, P1, P2, r, t, C8, Dq;
+  fe_quad<QP_0101>(S, V);     // X | Y | X | Y
+  fe_mul_rows2(R1, S, S, ~(m0 | m1));  // A = X^2 | B = Y^2 | . | .
+  fe_quad<QP_0>(Aq, R1);
+  fe_quad<QP_1100>(RA, R1);
+  fe_quad<QP_0112>(T, V);
+  fe_sel(opA, RA, T, m0 | m2);
+  fe_sel(opB, RA, V, m2);
+  fe_mul(R2, opA, opB);       // M | C | YZ | A^2
+  fe_quad<QP_3021>(P1, R2);
+  fe_quad<QP_0331>(P2, R2);
+  const uint32_t k1 = m0 ? 9u : (m1 ? 36u : (m2 ? 2u : 0u));
+  const uint32_t k2 = m0 ? 8u : (m1 ? 27u : (m2 ? 0u : 8u));
+  fe_lin2(r, P1, k1, P2, k2); // X3 | D | Z3 | -8C
+  fe_quad<QP_3>(C8, r);
+  fe_quad<QP_1>(Dq, r);       // D on every lane
+  fe_mul_rows4(t, Aq, Dq, m0, m1, m2);
+  fe_add(t, t, C8);           // . | Y3 = A D - 8C | . | .
+  fe_sel(V, r, t, m1);
+}
+
 struct Stamp { unsigned long long t0, t1, r0, r1; };
 
 __device__ void seed_point(uint32_t c, gej& p) {
@@ -94,11 +170,15 @@ __global__ void check_forms(uint32_t* bad) {
     fe V = p.z;
     fe_sel(V, V, p.y, m1);
     fe_sel(V, V, p.x, m0);
+    fe V2 = V;
     for (int d = 0; d < NDBL; ++d) quad_double(V, m0, m1, m2);
     const int b4 = (int)(ln & ~3u);
     gej q;
     q.x = shfl_fe(V, b4); q.y = shfl_fe(V, b4 + 1); q.z = shfl_fe(V, b4 + 2);
     if (!same_point(q, ref)) nb |= 1u;
+    for (int d = 0; d < NDBL; ++d) quad_double_split(V2, m0, m1, m2);
+    q.x = shfl_fe(V2, b4); q.y = shfl_fe(V2, b4 + 1); q.z = shfl_fe(V2, b4 + 2);
+    if (!same_point(q, ref)) nb |= 8u;
   }
   // 2M + 5S against 3M + 4S
   {
@@ -154,7 +234,9 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, Stamp* st) {
       if constexpr (OP == 5) gej_double(g, g);
       else gej_double_2m5s(g, g);
       V = g.x; b = g.y; Z = g.z;
-    }
+    } else if constexpr (OP == 7) quad_double_split(V, m0, m1, m2);
+    else if constexpr (OP == 8) fe_mul_rows2(V, V, V, ~(m0 | m1));
+    else if constexpr (OP == 9) fe_mul_rows4(V, V, b, m0, m1, m2);
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
   unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -166,7 +248,7 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, Stamp* st) {
 }
 
 static const char* NAMES[] = {"quad_double", "pair_double", "fe_sqr", "fe_mul", "fe_sub", "gej_double (3M+4S)",
-                              "gej_double_2m5s"};
+                              "gej_double_2m5s", "quad_double_split", "fe_mul_rows2 (square)", "fe_mul_rows4"};
 
 template <int OP>
 void run(int n_cu, int wps = 1) {
@@ -209,9 +291,10 @@ int main() {
   uint32_t hb = 0;
   hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
   printf("{\"check\": \"quad/pair doubling forms vs gej_double, %d doublings (bit 0 quad, 1 pair, 2 the 2M + 5S form)\", "
-         "\"lanes\": %d, \"fail_mask\": %u}\n", NDBL, 256 * 256, hb);  // bit 2: 2M + 5S
+         "\"lanes\": %d, \"fail_mask\": %u}\n", NDBL, 256 * 256, hb);  // bit 2: 2M + 5S, bit 3: quad split
   hipFree(bad);
   run<0>(n_cu); run<1>(n_cu); run<2>(n_cu); run<3>(n_cu); run<4>(n_cu);
   run<5>(n_cu); run<6>(n_cu); run<5>(n_cu, 4); run<6>(n_cu, 4);  // the ecmult kernel runs 4 waves/SIMD
+  run<7>(n_cu); run<8>(n_cu); run<9>(n_cu);
   return hb ? 1 : 0;
 }
