@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(WG) hkv_header_kernel(const uint32_t* __restri
 }
 
 // ---------------------------------------------------------------------------
-// Block merkle roots (DESIGN.md §8 next-4). The reference's own block test
+// Block merkle roots (DESIGN.md §4.5). The reference's own block test
 // asserts b.header.merkle == buildMerkleRoot (txHash <$> b.txs)
 // (/root/reference/test/Haskoin/NodeSpec.hs:185-193) on blocks fetched by
 // getBlocks (src/Haskoin/Node/Peer.hs:309-344); buildMerkleRoot is

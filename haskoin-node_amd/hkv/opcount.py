@@ -42,7 +42,7 @@ YFREE = True         # full-grid batches verify y-free (hkv_layout.h HKV_YFREE)
 def ecmult_products(qw: int = QW, beta_per_lookup: bool = False) -> int:
     """The ecmult stage: hkv_ecmult_kernel, plus (y-free) the finish and
     verdict kernels that complete u1*G + u2*Q and decide x(R) == r.
-    qw / beta_per_lookup price the variants (DESIGN.md §4 Roofline, floor):
+    qw / beta_per_lookup price the variants (the floor):
     radix-2^qw Q windows, and an (x, y)-only Q table whose lambda lookups
     form beta * x per addition instead of storing it."""
     q_table = 1 << (qw - 1)

@@ -24,7 +24,7 @@ What it restates. None of these functions lives i
 * ``verify_hash_sig``   — haskoin-core ``Haskoin.Crypto.Signature.verifyHashSig``
   (a1): normalize to low-S FIRST, then verify (so high-S is accepted).
 
-Parity status (DESIGN.md §Oracle): the reference's own fixtures
+Parity status (DESIGN.md §2): the reference's own fixtures
 (``test/Haskoin/NodeSpec.hs:282-340``) contain no signatures, so ECDSA verdict
 parity is UNPINNED by the reference. This oracle is cross-checked against
 OpenSSL 3.0.2 ``ECDSA_do_verify`` on the classes where the semantics agree

@@ -1,5 +1,5 @@
 """The roofline numerator and the product-count pricing of kernel variants
-(hkv/opcount.py; DESIGN.md §4 Roofline)."""
+(hkv/opcount.py)."""
 from hkv import opcount as oc
 
 

@@ -4,7 +4,7 @@
 // against the primitive's VALU instruction count (the issue-bound floor).
 //
 // Ops 7-10 are the representation study (results in
-// profiles/r02_ubench_field*.json and DESIGN.md §4): a 9 x 29-bit limb field
+// profiles/r02_ubench_field*.json and profiles/DESIGN_history_r01_r04.md §4): a 9 x 29-bit limb field
 // (tools/fe29_proto.h: carry-free v_mad_u64_u32 columns) and a lower bound
 // for 52-bit limbs on v_fma_f64 (only the 5 x 5 product with the exact
 // hi/lo split and integer column accumulation — no normalisation, no
