@@ -2562,10 +2562,22 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
       if (k < n3k) {
         key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), k * T + threadIdx.x, n_keys, a.kbits);
       } else {
-        const uint32_t base = (k - n3k) * PAIR_SIGS, shift = base - sbase;  // record = slot + shift
-        pair_group<false>(sbase, a.im, n_cand - shift, slots, a.gtab, a.cbits + shift / 32, 0xFFFFFFFFu, a.aux,
-                          reinterpret_cast<uint32_t*>(a.cand) + (size_t)shift * REC_WORDS, HKV_MODE_HASKOIN,
-                          nullptr, none, qlds, hlds, xch, buf);
+        // the group's records [base, base + 32) run on this workgroup's own
+        // scratch slots [sbase, sbase + 32): pair_group indexes records and
+        // verdict words by slot, so both are handed over shifted by
+        // base - sbase, which is negative when the group lies below the slot
+        // (a queue hands any group to any workgroup) — formed on the 64-bit
+        // address as an integer, never as an out-of-range pointer, and every
+        // access lands at base + lane >= 0
+        const uint32_t base = (k - n3k) * PAIR_SIGS;
+        const int64_t shift = (int64_t)base - (int64_t)sbase;  // a multiple of 32
+        uint32_t* recs = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(a.cand) +
+                                                     (uintptr_t)(shift * (int64_t)(REC_WORDS * 4)));
+        uint32_t* bits = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(a.cbits) +
+                                                     (uintptr_t)(shift / 32 * 4));
+        // slot i is record i + shift: valid iff i + shift < n_cand (mod 2^32: n_cand - shift < 2^32)
+        pair_group<false>(sbase, a.im, (uint32_t)((int64_t)n_cand - shift), slots, a.gtab, bits, 0xFFFFFFFFu, a.aux,
+                          recs, HKV_MODE_HASKOIN, nullptr, none, qlds, hlds, xch, buf);
       }
     } else {
       // 4. the countMulSig walk
