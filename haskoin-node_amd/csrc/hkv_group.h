@@ -335,7 +335,85 @@ constexpr int QP_0331 = 0x7C;                                   // [0,3,3,1]
 // quad permutation of a product are formed by a single DPP move per limb
 // (P1, P2), and the others by two permutations and one select, not by
 // broadcasts and select chains.
+#ifndef HKV_QUAD_SPLIT  // 1: quad_double's lane-idle products spread over the quad (fe_mul_rows2 / 4)
+#define HKV_QUAD_SPLIT 0
+#endif
+template <int PERM>
+HKV_DEV uint32_t dpp_quad(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, PERM, 0xF, 0xF, false);
+}
+constexpr int QP_X2 = 0x4E, QP_X1 = 0xB1, QP_0101 = 0x44, QP_1 = 0x55;  // [2,3,0,1] [1,0,3,2] [0,1,0,1] [1,1,1,1]
+// Lane-split products: the 64 limb products of one 256 x 256 product spread
+// by rows of a over the lanes of a quad, the partial products summed across
+// lanes by DPP, one reduction. For the products of quad_double that would
+// otherwise leave lanes of the quad idle.
+// r = a b on the lane with hsel = 0 of the pair {q, q ^ 2}; the partner
+// (hsel = all ones) takes a's rows 4..7. Same a, b on both lanes.
+HKV_DEV void fe_mul_rows2(fe& r, const fe& a, const fe& b, uint32_t hsel) {
+  uint32_t ar[4], p[12], t[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ar[k] = (a.v[k] & ~hsel) | (a.v[k + 4] & hsel);
+  mul4x8_ps(p, ar, b.v);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = p[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[4 + k] = addc(p[4 + k], dpp_quad<QP_X2>(p[k]), c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[12 + k] = addc(0u, dpp_quad<QP_X2>(p[8 + k]), c);
+  fe_reduce512(r, t);
+}
+// r = a b on quad lane 1: rows 0,1 of a on lane 1, 2,3 on lane 0, 4,5 on
+// lane 3, 6,7 on lane 2 (m0 / m1 / m2: all ones on quad lane 0 / 1 / 2);
+// the same b on every lane
+HKV_DEV void fe_mul_rows4(fe& r, const fe& a, const fe& b, uint32_t m0, uint32_t m1, uint32_t m2) {
+  const uint32_t m3 = ~(m0 | m1 | m2);
+  uint32_t ar[2], p[10], t1[12], t[16];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    ar[k] = (a.v[k] & m1) | (a.v[2 + k] & m0) | (a.v[4 + k] & m3) | (a.v[6 + k] & m2);
+  mul2x8_ps(p, ar, b.v);
+  uint32_t c = 0;
+  t1[0] = p[0];
+  t1[1] = p[1];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t1[2 + k] = addc(p[2 + k], dpp_quad<QP_X1>(p[k]), c);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) t1[10 + k] = addc(0u, dpp_quad<QP_X1>(p[8 + k]), c);
+  c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = t1[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[4 + k] = addc(t1[4 + k], dpp_quad<QP_X2>(t1[k]), c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[12 + k] = addc(0u, dpp_quad<QP_X2>(t1[8 + k]), c);
+  fe_reduce512(r, t);
+}
+
 HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
+#if HKV_QUAD_SPLIT
+  // [A | B] as two 2-way row-split squares (X^2 on lanes 0, 2; Y^2 on 1, 3),
+  // Y3 = A D - 8C as one 4-way row-split product landing on lane 1
+  fe S, R1, Aq, RA, T, opA, opB, R2, P1, P2, r, t, C8, Dq;
+  fe_quad<QP_0101>(S, V);     // X | Y | X | Y
+  fe_mul_rows2(R1, S, S, ~(m0 | m1));  // A = X^2 | B = Y^2 | . | .
+  fe_quad<QP_0>(Aq, R1);      // A        | A      | A  | A
+  fe_quad<QP_1100>(RA, R1);   // B        | B      | A  | A
+  fe_quad<QP_0112>(T, V);     // X        | .      | Y  | .
+  fe_sel(opA, RA, T, m0 | m2);    // X | B | Y | A
+  fe_sel(opB, RA, V, m2);         // B | B | Z | A
+  fe_mul(R2, opA, opB);       // M | C | YZ | A^2
+  fe_quad<QP_3021>(P1, R2);   // A^2 | M | YZ | C
+  fe_quad<QP_0331>(P2, R2);   // M | A^2 | . | C
+  const uint32_t k1 = m0 ? 9u : (m1 ? 36u : (m2 ? 2u : 0u));
+  const uint32_t k2 = m0 ? 8u : (m1 ? 27u : (m2 ? 0u : 8u));
+  fe_lin2(r, P1, k1, P2, k2); // X3 | D = 36M - 27A^2 | Z3 = 2YZ | -8C
+  fe_quad<QP_3>(C8, r);       // -8C on every lane
+  fe_quad<QP_1>(Dq, r);       // D on every lane
+  fe_mul_rows4(t, Aq, Dq, m0, m1, m2);
+  fe_add(t, t, C8);           // . | Y3 = A D - 8C | . | .
+  fe_sel(V, r, t, m1);        // X3 | Y3 | Z3 | .
+#else
   fe R1, Aq, RA, T, opA, opB, R2, P1, P2, r, t, C8;
   fe_sqr(R1, V);              // A = X^2 | B = Y^2 | . | .
   fe_quad<QP_0>(Aq, R1);      // A        | A      | A  | A
@@ -352,6 +430,7 @@ HKV_DEV void quad_double(fe& V, uint32_t m0, uint32_t m1, uint32_t m2) {
   fe_quad<QP_3>(C8, r);       // -8C on every lane
   fe_mul_add(t, Aq, r, C8);   // . | Y3 = A D - 8C | . | .
   fe_sel(V, r, t, m1);        // X3 | Y3 | Z3 | .
+#endif
 }
 
 // P += TXY in place for a table build: TXY affine on the curve of the

@@ -2,7 +2,8 @@
 # Round-5 session B: the lane-split product prototype (tools/ubench_chain:
 # correctness check, then lone-wave cycles), the multisig tail as an ordered
 # work queue (its GPU tests first, then the whole suite), and a same-box A/B
-# of the block legs against the grid-barrier tail (libhkv_base.so, HKV_LIB).
+# of the block legs against the grid-barrier tail (libhkv_base.so, HKV_LIB)
+# and the lane-split quad doubling (libhkv_qsplit.so, -DHKV_QUAD_SPLIT=1).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -18,8 +19,9 @@ B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-adversarial --no-header
 for k in 1 2; do
   HKV_LIB=haskoin-node_amd/lib/libhkv_base.so timeout -k 10 200 python $B > gpurun_out/${TAG}_base$k.log 2>&1 || exit 1
   timeout -k 10 200 python $B > gpurun_out/${TAG}_new$k.log 2>&1 || exit 1
+  HKV_LIB=haskoin-node_amd/lib/libhkv_qsplit.so timeout -k 10 200 python $B > gpurun_out/${TAG}_qsplit$k.log 2>&1 || exit 1
 done
-for f in gpurun_out/${TAG}_base1.log gpurun_out/${TAG}_new1.log gpurun_out/${TAG}_base2.log gpurun_out/${TAG}_new2.log; do
+for f in gpurun_out/${TAG}_{base,new,qsplit}{1,2}.log; do
   python3 - "$f" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

@@ -48,54 +48,7 @@ __device__ __forceinline__ void gej_double_2m5s(gej& r, const gej& a) {
 // ---- lane-split products (prototype): the 64 limb
 // products of one 256 x 256 product spread over 2 or 4 lanes of a quad by
 // rows of a, the partials summed across lanes by DPP, one reduction ----
-template <int PERM>
-__device__ __forceinline__ uint32_t dppq(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, PERM, 0xF, 0xF, false);
-}
-constexpr int QP_X2 = 0x4E, QP_X1 = 0xB1, QP_0101 = 0x44, QP_1 = 0x55;  // [2,3,0,1] [1,0,3,2] [0,1,0,1] [1,1,1,1]
-// r = a * b on the lane with hsel = 0 of the pair {q, q ^ 2}; its partner
-// (hsel = all ones) takes a's rows 4..7. Same a, b on both lanes.
-__device__ __forceinline__ void fe_mul_rows2(fe& r, const fe& a, const fe& b, uint32_t hsel) {
-  uint32_t ar[4], p[12], t[16];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) ar[k] = (a.v[k] & ~hsel) | (a.v[k + 4] & hsel);
-  mul4x8_ps(p, ar, b.v);
-  uint32_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) t[k] = p[k];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t[4 + k] = addc(p[4 + k], dppq<QP_X2>(p[k]), c);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) t[12 + k] = addc(0u, dppq<QP_X2>(p[8 + k]), c);
-  fe_reduce512(r, t);
-}
-// r = a * b on quad lane 1: rows 0,1 on lane 1, 2,3 on lane 0, 4,5 on lane
-// 3, 6,7 on lane 2 (m0 / m1 / m2 all ones on quad lane 0 / 1 / 2); same b on
-// every lane
-__device__ __forceinline__ void fe_mul_rows4(fe& r, const fe& a, const fe& b, uint32_t m0, uint32_t m1,
-                                             uint32_t m2) {
-  const uint32_t m3 = ~(m0 | m1 | m2);
-  uint32_t ar[2], p[10], t1[12], t[16];
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-    ar[k] = (a.v[k] & m1) | (a.v[2 + k] & m0) | (a.v[4 + k] & m3) | (a.v[6 + k] & m2);
-  mul2x8_ps(p, ar, b.v);
-  uint32_t c = 0;
-  t1[0] = p[0];
-  t1[1] = p[1];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t1[2 + k] = addc(p[2 + k], dppq<QP_X1>(p[k]), c);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) t1[10 + k] = addc(0u, dppq<QP_X1>(p[8 + k]), c);
-  c = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) t[k] = t1[k];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t[4 + k] = addc(t1[4 + k], dppq<QP_X2>(t1[k]), c);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) t[12 + k] = addc(0u, dppq<QP_X2>(t1[8 + k]), c);
-  fe_reduce512(r, t);
-}
+// fe_mul_rows2 / fe_mul_rows4: hkv_group.h (HKV_QUAD_SPLIT)
 // quad_double with the two products that leave lanes idle spread over them:
 // [A | B] as two 2-way row-split squares (X^2 on lanes 0, 2; Y^2 on 1, 3),
 // Y3 = A D - 8C as a 4-way row-split product on lane 1
