@@ -96,6 +96,8 @@ struct DevCtx {
   // previous user's work (this event) before enqueueing and records it after,
   // so calls on different streams run in enqueue order instead of racing.
   hipEvent_t last_use = nullptr;
+  hipStream_t last_stream = nullptr;  // the stream last_use was recorded on (valid: last_valid)
+  bool last_valid = false;
   uint32_t inject = 0;  // hkv_debug_fail_device: HKV_FAIL_* of this device's next host-batch shard
 };
 
@@ -177,11 +179,17 @@ int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
 // Order a call on stream st after the previous user of the device's scratch
 // (acquire) and publish st as the new last user (release). Callers hold ctx->mu.
 int scratch_acquire(DevCtx& d, hipStream_t st) {
+  // (a call on the stream of the last release is ordered after it already:
+  // one HIP call less in front of a block's first launch)
+  if (d.last_valid && st == d.last_stream) return HKV_OK;
   HKV_TRY(hipStreamWaitEvent(st, d.last_use, 0), "hipStreamWaitEvent(scratch)");
   return HKV_OK;
 }
 int scratch_release(DevCtx& d, hipStream_t st) {
+  d.last_valid = false;
   HKV_TRY(hipEventRecord(d.last_use, st), "hipEventRecord(scratch)");
+  d.last_stream = st;
+  d.last_valid = true;
   return HKV_OK;
 }
 
