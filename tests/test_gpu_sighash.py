@@ -909,3 +909,60 @@ def test_block_kernel_malformed_wire_vs_oracle(torch, ver, coracle, forkid):
     got = unpack_bits(words, len(arr)).tolist()
     check(got[:len(jobs)])
     assert got[len(jobs):] == [False, False]
+
+
+def test_block_kernel_random_wire_mutations_vs_oracle(torch, ver, coracle):
+    """Random byte-level damage to signed txs (a byte flipped, inserted or
+    deleted at a random position, the tail cut, two txs spliced), 1,500
+    mutants in one block-sized batch beside their intact originals, through
+    both standard-input entry points: every verdict equals the oracle's
+    (a tx that no longer parses rejects) and every record the block kernel
+    wrote equals the oracle's. Complements the structured malformed-wire
+    cases with positions the structure does not pick."""
+    import hkv
+    rng = random.Random(0xF022)
+    keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(8)]
+    txs, jobs = txgen.std_block(rng, 120, keys, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
+    raw = [sh.tx_serialize(t) for t in txs]
+    all_raw, all_jobs, kinds = list(raw), list(jobs), ["valid"] * len(jobs)
+    for _ in range(1500):
+        t, i, p, v = rng.choice(jobs)
+        b = bytearray(raw[t])
+        k = rng.randrange(6)
+        pos = rng.randrange(len(b))
+        if k == 0:
+            b[pos] ^= 1 << rng.randrange(8)
+        elif k == 1:
+            b.insert(pos, rng.randrange(256))
+        elif k == 2:
+            del b[pos]
+        elif k == 3:
+            b = b[:pos]
+        elif k == 4:
+            b[pos] = rng.choice([0x00, 0xFD, 0xFE, 0xFF])
+        else:
+            other = raw[rng.randrange(len(raw))]
+            b = b[:pos] + other[rng.randrange(len(other)):]
+        all_raw.append(bytes(b))
+        all_jobs.append((len(all_raw) - 1, i, p, v))
+        kinds.append(("flip", "insert", "delete", "cut", "varint", "splice")[k])
+    assert len(all_jobs) <= 16 * 256
+    parsed = []
+    for b in all_raw:
+        try:
+            parsed.append(sh.tx_parse(b))
+        except (ValueError, IndexError):
+            parsed.append(None)
+    exp = []
+    for (t, i, p, v) in all_jobs:
+        tx = parsed[t]
+        ok = tx is not None and i < len(tx.inputs)
+        exp.append(sh.std_input_record(tx, i, p, v, None) if ok else b"\0" * 168)
+    want = oracle_batch(coracle, b"".join(exp), 1).tolist()
+    assert all(want[:len(jobs)]) and sum(not w for w in want) > 1000
+    got, recs = _device_verify_std(torch, ver, all_raw, all_jobs, None, records=True)
+    bad = [(kinds[k], got[k], want[k]) for k in range(len(all_jobs)) if got[k] != want[k]]
+    assert not bad, bad[:10]
+    badr = [kinds[k] for k in range(len(all_jobs)) if recs[k * 168:(k + 1) * 168] != exp[k]]
+    assert not badr, badr[:10]
+    assert hkv.verify_std_inputs(ver, all_raw, all_jobs) == want
