@@ -714,7 +714,13 @@ def load_traffic(path: str, n: int):
     f, w = tj.get("fetch_bytes_per_launch"), tj.get("write_bytes_per_launch")
     if f is None or w is None:
         return None, None
-    return 2 * f + w, {"fetch_size_bytes": f, "write_size_bytes": w, "source": tj.get("source")}
+    raw = {"fetch_size_bytes": f, "write_size_bytes": w, "source": tj.get("source")}
+    # VALU busy, occupancy and the integer instruction counts of
+    # the same profiled launch
+    for k in ("valu_busy_pct", "waves_per_simd", "SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"):
+        if k in tj:
+            raw[k] = tj[k]
+    return 2 * f + w, raw
 
 
 def _free_port() -> int:

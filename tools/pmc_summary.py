@@ -91,6 +91,20 @@ def main(src: str, dst: str) -> None:
              "hbm_bytes_per_launch": (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024,
              "source": os.path.relpath(dst), "hbm_bytes_per_launch_corrected": (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024,
              "note": "raw FETCH_SIZE / WRITE_SIZE (KB*1024), separate pmc passes; corrected = 2 x FETCH + WRITE"}
+        # VALU busy and occupancy of the same launch. VALUBusy =
+        # SQ_ACTIVE_INST_VALU x 4 cycles / (SIMDs x GRBM_GUI_ACTIVE per XCD);
+        # the wave count over the SIMDs is the resident waves per SIMD (the
+        # grid is sized to exactly one resident round: grid-stride)
+        n_simd, n_xcd = 1024, 8
+        if "SQ_ACTIVE_INST_VALU" in e and "GRBM_GUI_ACTIVE" in e:
+            gui = e["GRBM_GUI_ACTIVE"] / n_xcd
+            t["valu_busy_pct"] = round(100.0 * e["SQ_ACTIVE_INST_VALU"] * 4 / n_simd / gui, 1)
+            t["grbm_gui_active_per_xcd"] = gui
+        if "SQ_WAVES" in e:
+            t["waves_per_simd"] = round(e["SQ_WAVES"] / n_simd, 2)
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"):
+            if c in e:
+                t[c] = e[c]
         json.dump(t, open(os.path.join(os.path.dirname(dst.rstrip("/")), "latest_pmc_traffic.json"), "w"), indent=1)
     print(json.dumps({k: {c: "%.4g" % v for c, v in d.items()} for k, d in out.items()}, indent=1))
 
