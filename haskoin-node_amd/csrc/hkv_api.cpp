@@ -71,14 +71,14 @@ struct DevCtx {
   // records, [5] key-check verdict words, [6] host-form verdict words
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
-  void* ms_ctr = nullptr;            // scan counters: [0] running sum (the tail reads and re-arms it)
-  // the tail kernel's words: [0..7] and [8..15] the two work-queue slots
-  // (claim, done per phase; launch `tail_epoch` uses slot tail_epoch & 1 and
-  // zeroes the other), [16] the sticky fault latch (hkv_device_fault), [17]
-  // the host form's per-call status word
+  void* ms_ctr = nullptr;            // scan sums: [epoch & 1] this call's (its tail launch zeroes the other)
+  // the tail's words: [0..7] and [8..15] the two work-queue slots (claim,
+  // done per phase; launch `tail_epoch` uses slot tail_epoch & 1 and zeroes
+  // the other), [16] the sticky fault latch (hkv_device_fault), [17] the host
+  // form's per-call status word
   unsigned int* ms_bar = nullptr;
   uint32_t tail_epoch = 0;
-  bool inject_tail = false;          // hkv_debug_fail_device(HKV_FAIL_TAIL): the next tail launch's barriers give up
+  bool inject_tail = false;          // hkv_debug_fail_device(HKV_FAIL_TAIL): the next tail's phase waits give up
   uint32_t* call_status = nullptr;   // the current call's status word (device; HKV_STATUS_* ORed in), or null
   bool ms_dirty = false;             // a call failed after its scan launch: zero ms_ctr before the next scan
   uint32_t* rare_ctr = nullptr;      // y-free rare-lane count (hkv_finish_kernel appends, hkv_yverdict_kernel re-arms)
@@ -313,8 +313,7 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming), "hipEventCreate(join)");
   HKV_TRY(hipEventCreateWithFlags(&d.last_use, hipEventDisableTiming), "hipEventCreate(scratch)");
   HKV_TRY(hipEventRecord(d.last_use, d.stream), "hipEventRecord(scratch)");
-  // the multisig scan's running sum (the tail kernel reads and re-arms it);
-  // the tail's barrier words
+  // the multisig scan's two parity sums; the tail's queue words
   HKV_TRY(hipMalloc(&d.ms_ctr, 4 * sizeof(uint64_t)), "hipMalloc(multisig counters)");
   HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 4 * sizeof(uint64_t), d.stream), "hipMemset(multisig counters)");
   HKV_TRY(hipMalloc(reinterpret_cast<void**>(&d.ms_bar), MS_BAR_WORDS * sizeof(unsigned int)), "hipMalloc(multisig barrier)");
@@ -497,6 +496,44 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
 int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                      uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
                      const hkv::MsScan& ms, size_t cap_cand);
+// the multisig tail's operands for this call (launch epoch d.tail_epoch)
+hkv::MsTail tail_args(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
+                      uint32_t* out_bits, bool fused, const hkv::MsScan& ms, size_t cap_cand) {
+  uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
+  uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr);
+  hkv::MsTail t;
+  t.txs = dt->bytes;
+  t.tx_off = dt->offsets;
+  t.n_tx = dt->n_tx;
+  t.txt = d.txt;
+  t.scripts = dt->scripts;
+  t.scripts_len = dt->scripts_len;
+  t.jobs = jobs;
+  t.n = (uint32_t)n;
+  t.forkid = forkid;
+  // the fused launch's index hashed nothing: the multisig sighashes need the
+  // BIP143 per-tx hashes the network allows (the extraction path built them)
+  t.hash_txs = fused ? std_tx_hashes(forkid) : hkv::TX_HASHES_NONE;
+  t.desc = ms.desc;
+  t.off = ms.off;
+  t.total = reinterpret_cast<unsigned long long*>(ms.counters);
+  t.total_next = reinterpret_cast<unsigned long long*>(ctr + ((d.tail_epoch + 1u) & 1u));
+  t.cand = cand;
+  t.keyrec = cand + cap_cand * hkv::REC_SIZE;
+  t.cbits = static_cast<uint32_t*>(d.ms[3]);
+  t.kbits = static_cast<uint32_t*>(d.ms[5]);
+  t.im = d.im;
+  t.aux = d.aux;
+  t.gtab = d.gtab;
+  t.qs = d.qs;
+  t.out_bits = out_bits;
+  t.bar = d.ms_bar;
+  t.epoch = d.tail_epoch;
+  t.fault = d.ms_bar + MS_FAULT;
+  t.status = d.call_status;
+  t.force_fault = d.inject_tail ? 1u : 0u;
+  return t;
+}
 int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                       uint32_t* out_bits, hipStream_t st) {
   const bool fused = split_batch(d, n);
@@ -517,11 +554,13 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   uint32_t* desc = static_cast<uint32_t*>(d.ms[0]);
   uint64_t* off = static_cast<uint64_t*>(d.ms[2]);
   if (d.ms_dirty) {  // an earlier call failed after its scan launch: counters may be stale
-    HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 3 * sizeof(uint64_t), st), "hipMemset(multisig counters)");
+    HKV_TRY(hipMemsetAsync(d.ms_ctr, 0, 2 * sizeof(uint64_t), st), "hipMemset(multisig counters)");
     d.ms_dirty = false;
   }
   d.ms_dirty = true;  // until this call's tail is enqueued
-  uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr);
+  // this call's scan sum: the parity word of its tail epoch (the launch that
+  // runs the tail zeroes the other one for the next call)
+  uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr) + (d.tail_epoch & 1u);
   const hkv::MsScan ms{desc, off, ctr};
   // Larger batches (HKV_STD_OVERLAP): the index rows on st, then the hash
   // half (BIP143 per-tx hashes, the script checks and the sighashes, writing
@@ -583,13 +622,10 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
 int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                      uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
                      const hkv::MsScan& ms, size_t cap_cand) {
-  uint32_t* desc = ms.desc;
-  uint64_t* off = ms.off;
-  uint64_t* ctr = ms.counters;
   int rc = HKV_OK;
   if (!fused_scan && !overlap)  // (the overlapped form scanned on the hash stream)
     HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
-                                desc, off, ctr, st),
+                                ms.desc, ms.off, ms.counters, st),
             "multisig scan launch");
   if (!fused) {
     const hkv::StdOps so{dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, forkid};
@@ -597,39 +633,10 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
                         overlap ? &so : nullptr);
     if (rc) return rc;
   }
-  uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
-  hkv::MsTail t;
-  t.txs = dt->bytes;
-  t.tx_off = dt->offsets;
-  t.n_tx = dt->n_tx;
-  t.txt = d.txt;
-  t.scripts = dt->scripts;
-  t.scripts_len = dt->scripts_len;
-  t.jobs = jobs;
-  t.n = (uint32_t)n;
-  t.forkid = forkid;
-  // the fused launch's index hashed nothing: the multisig sighashes need the
-  // BIP143 per-tx hashes the network allows (the extraction path built them)
-  t.hash_txs = fused ? std_tx_hashes(forkid) : hkv::TX_HASHES_NONE;
-  t.desc = desc;
-  t.off = off;
-  t.total = reinterpret_cast<unsigned long long*>(ctr);
-  t.cand = cand;
-  t.keyrec = cand + cap_cand * hkv::REC_SIZE;
-  t.cbits = static_cast<uint32_t*>(d.ms[3]);
-  t.kbits = static_cast<uint32_t*>(d.ms[5]);
-  t.im = d.im;
-  t.aux = d.aux;
-  t.gtab = d.gtab;
-  t.qs = d.qs;
-  t.out_bits = out_bits;
-  t.bar = d.ms_bar;
-  t.epoch = d.tail_epoch;
-  t.fault = d.ms_bar + MS_FAULT;
-  t.status = d.call_status;
-  t.force_fault = d.inject_tail ? 1u : 0u;
-  HKV_TRY(hkv::launch_ms_tail(t, (uint32_t)d.n_cu, st), "multisig tail launch");
-  ++d.tail_epoch;  // (launched: it zeroes the slot the next launch uses)
+  // (operands taken after every launch before it has sized the scratch)
+  HKV_TRY(hkv::launch_ms_tail(tail_args(d, dt, jobs, n, forkid, out_bits, fused, ms, cap_cand), (uint32_t)d.n_cu, st),
+          "multisig tail launch");
+  ++d.tail_epoch;  // (launched: it zeroes the slot and the scan sum the next call uses)
   d.inject_tail = false;
   return HKV_OK;
 }
@@ -1188,8 +1195,8 @@ int hkv_verify_std_inputs(hkv_ctx* ctx, const hkv_txs* txs, const hkv_input_job*
   uint32_t fault = 0;
   HKV_TRY(hipMemcpyAsync(&fault, status, sizeof(fault), hipMemcpyDeviceToHost, d.stream), "D2H call status");
   HKV_TRY(hipStreamSynchronize(d.stream), "std inputs sync");
-  if (fault & HKV_STATUS_TAIL_FAULT) {  // the multisig tail's grid barrier gave up (its verdicts are incomplete)
-    g_last_hip = "multisig tail: grid barrier timed out (workgroups not co-resident)";
+  if (fault & HKV_STATUS_TAIL_FAULT) {  // a multisig tail queue wait gave up (its verdicts are incomplete)
+    g_last_hip = "multisig tail: work-queue wait timed out";
     (void)scratch_release(d, d.stream);
     return HKV_E_INTERNAL;
   }

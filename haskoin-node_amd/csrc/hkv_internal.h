@@ -33,15 +33,16 @@ hipError_t launch_ecmult(uint32_t* im, uint32_t n, uint32_t n_pad, const uint32_
                          hipStream_t st);
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st);
 // the multisig scan operands a fused launch may take over (hkv_ms_scan_kernel's);
-// counters: [0] the running sum (candidates | key checks << 32), which the tail
-// kernel reads after the scan and re-arms
+// counters: this call's running sum (candidates | key checks << 32), one of
+// two parity words (the call's tail epoch): the tail reads it after the scan,
+// and the launch that runs the tail zeroes the other word for the next call
 struct MsScan {
   uint32_t* desc;
   uint64_t* off;
   uint64_t* counters;
 };
-// The multisig tail (hkv_kernels.hip hkv_ms_tail_kernel): one launch after the
-// scan that does nothing when the batch has no multisig input and otherwise
+// The multisig tail (hkv_kernels.hip 2e): one launch after the scan that
+// does nothing when the batch has no multisig input and otherwise
 // the BIP143 per-tx hashes (hash_txs), the candidate / key-check records, the
 // key checks, the candidate verifies and the countMulSig walk — read from the
 // device total, so the host never waits for it.
@@ -58,7 +59,8 @@ struct MsTail {
   uint32_t hash_txs;  // TX_HASHES_* the tail computes first (the fused path's index hashed nothing)
   const uint32_t* desc;
   const uint64_t* off;
-  unsigned long long* total;        // MsScan counters[0]: the scan's running sum (the tail re-arms it)
+  unsigned long long* total;        // this call's scan sum (MsScan counters: ms_ctr[epoch & 1])
+  unsigned long long* total_next;   // the next call's (ms_ctr[(epoch + 1) & 1]): zeroed by this launch
   uint8_t* cand;                    // candidate records (capacity n * 136)
   uint8_t* keyrec;                  // key-check records (capacity n * 16)
   uint32_t* cbits;                  // candidate verdict words
@@ -68,7 +70,8 @@ struct MsTail {
   const uint32_t* gtab;
   uint32_t* qs;
   uint32_t* out_bits;               // the batch's verdict words (multisig inputs are ORed in)
-  unsigned int* bar;                // two work-queue slots of 8 words (claim, done[4]): launch `epoch` uses slot epoch & 1
+  unsigned int* bar;                // two work-queue slots of 8 words (claim, done[4]): launch `epoch` uses
+                                    // slot epoch & 1 and zeroes the other
   uint32_t epoch;                   // this launch's sequence number on the device
   unsigned int* fault;              // the device's sticky fault latch (hkv_device_fault)
   uint32_t* status;                 // the call's status word (HKV_STATUS_* ORed in), or null

@@ -1602,13 +1602,13 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
     const int w_hi = wv == 0 ? BLK_K1 - 1 : (wv == 1 ? NWIN - 1 : BLK_K2 - 1);
     const int w_lo = wv == 0 ? 0 : (wv == 1 ? BLK_K2 : BLK_K1);
+    fe zs;  // the segment's isomorphic scale (formed before the chain: off the join's path)
+    fe_mul(zs, Zg, zb);
     bool inf;
     pair_chain(P, Z, inf, qlds[slot], im, n_pad, i, valid, negh, half, odd, ln, w_hi, w_lo);
     mark(wv == 0 ? STAMP_CHAIN0 : (wv == 1 ? STAMP_CHAIN1 : STAMP_CHAIN_MID));
     fe Zs;
     halves_sum(xch[slot], c, half, odd, P, Z, inf, Zs);  // S = P | Zs on E_w at scale Zg * zb
-    fe zs;
-    fe_mul(zs, Zg, zb);
     if (wv == 0) {
       // ---- T = A + phi^-1(S_lo) on E (A = u1 G, y0 the key's y) ----
       blk_wait(&bflag[BF_A], seq);
@@ -1628,14 +1628,22 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       blk_post(&bflag[BF_T], seq);
     } else if (wv == 3) {
       // ---- U = T + phi^-1(S_mid) on E ----
-      blk_wait(&bflag[BF_T], seq);
+      // (S_mid's Z on E is formed before T arrives: y0 was published by this
+      // wave before its chain)
+      fe zbs;
       if (half == 0) {
-        fe PT, ZT, y0;
-        bool tinf;
+        fe y0, zt;
 #pragma unroll
         for (int k = 0; k < 8; ++k) y0.v[k] = aux[(size_t)(AUX_Y0 + k) * n_pad + i];
+        fe_mul(zt, Zs, zs);
+        fe_mul(zbs, zt, y0);
+      }
+      blk_wait(&bflag[BF_T], seq);
+      if (half == 0) {
+        fe PT, ZT;
+        bool tinf;
         pair_from_xch(xch[3], c, odd, PT, ZT, tinf);
-        add_segment(PT, ZT, tinf, P, Zs, inf, zs, y0, odd);
+        pair_add_var(PT, ZT, tinf, P, zbs, inf, odd);
         pair_to_xch(xch[4], c, odd, PT, ZT, tinf);
       }
       blk_post(&bflag[BF_U], seq);
@@ -2436,7 +2444,7 @@ namespace hkv {
 //     its record ranges and the batch total (candidates | key checks << 32)
 //     on the device. This one launch follows it on the stream, so the host
 //     never reads the total: with no multisig input every workgroup returns
-//     at once; otherwise, separated by grid barriers,
+//     at once; otherwise, in four phases,
 //       1. (fused paths, whose index pass hashed nothing) the BIP143 per-tx
 //          hashes of the batch's txs into their index rows;
 //       2. per input, its key-check records and, per signature, its sighash
@@ -2460,9 +2468,12 @@ namespace hkv {
 //     bounded anyway (~seconds, far above one item): a workgroup that gives
 //     up leaves the verdicts it owns at 0 (reject, never a false accept) and
 //     reports HKV_STATUS_TAIL_FAULT through the device's sticky latch and the
-//     call's status word. Each launch counts in its own slot (the epoch's
-//     parity) and zeroes the other for the next launch, so nothing a faulted
-//     launch leaves behind reaches a later one.
+//     call's status word. Each call counts in its own queue slot and scan
+//     sum (the parity of its tail epoch) and its tail zeroes the other pair
+//     for the next call, so nothing a faulted launch leaves behind reaches a
+//     later one. (The tail inside the block kernel instead — groups claimed
+//     from the queue, the tail's items after them — saved this launch but
+//     cost ~15 us per block: profiles/r05e/fused_tail_ab.txt.)
 // ---------------------------------------------------------------------------
 enum : uint32_t { TQ_CLAIM = 0, TQ_DONE = 1, TQ_SLOT = 8 };  // slot words: claim, done[4]
 // wait (thread 0) until `done` reaches `want`; false on a timeout (fault reported)
@@ -2479,6 +2490,14 @@ HKV_DEV bool tail_wait(const MsTail& a, unsigned int* done, uint32_t want) {
   }
   return true;
 }
+// an item's writes published, then its count: every wave waits for its own
+// stores (a barrier does not), then one agent-scope release (the XCD's L2
+// write-back) with the count
+HKV_DEV void publish_count(unsigned int* ctr) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
   __shared__ QLane qlds[2];
@@ -2486,17 +2505,17 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
   __shared__ uint32_t xch[25 * PAIR_SIGS];
   __shared__ uint32_t buf[16 * PAIR_TPB];  // sha256_stream blocks ([word][thread])
   __shared__ uint32_t item_s, go_s;
-  // this launch's queue slot (zeroed by the launch before it on the device's
-  // ordered stream of calls); the other slot is the next launch's
+  // this launch's queue slot and scan sum (zeroed by the launch before this
+  // one on the device's ordered stream of calls); workgroup 0 zeroes the
+  // other slot and sum, the next launch's
   unsigned int* q = a.bar + (a.epoch & 1u) * TQ_SLOT;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     unsigned int* nx = a.bar + ((a.epoch + 1u) & 1u) * TQ_SLOT;
 #pragma unroll
     for (int k = 0; k < (int)TQ_SLOT; ++k) __hip_atomic_store(&nx[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.total_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // the scan's running sum (final: the scan ran before this launch on the
-  // stream); re-armed by whichever workgroup completes the last item (or gives
-  // up): a workgroup starting after that reads 0 and has nothing to do
+  // the scan's sum: final (the scan ran before this launch on the stream)
   const unsigned long long total = __hip_atomic_load(a.total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
   if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid
@@ -2518,8 +2537,8 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
       // phase order, so only running items can be outstanding)
       const uint32_t need[4] = {0u, n1, n2, n3};
       if (ok && ph > seen) {
-        ok = tail_wait(a, &q[TQ_DONE + ph - 1], need[ph]) ? 1u : 2u;
-        if (ok == 1u) seen = ph;
+        ok = tail_wait(a, &q[TQ_DONE + ph - 1], need[ph]) ? 1u : 0u;
+        if (ok) seen = ph;
       }
       item_s = it;
       go_s = ok;
@@ -2527,11 +2546,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
     __syncthreads();
     const uint32_t it = item_s, go = go_s;
     __syncthreads();
-    if (go != 1u) {
-      if (go == 2u && threadIdx.x == 0)  // gave up: re-arm the scan sum for the next call
-        __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
+    if (!go) return;
     int ph;
     if (it < e1) {
       // 1. the BIP143 per-tx hashes (lanes hash-major, so a wave mostly
@@ -2585,15 +2600,10 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
       const uint32_t jx = (it - e3) * T + threadIdx.x;
       ms_resolve_lane(a.desc, a.off, jx, jx < a.n, a.cbits, a.kbits, a.out_bits);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      const uint32_t d = atomicAdd(&q[TQ_DONE + ph], 1u) + 1u;
-      if (ph == 3 && d == n4)  // the launch's last item: re-arm the scan sum
-        __hip_atomic_store(a.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    publish_count(&q[TQ_DONE + ph]);
   }
 }
+
 
 }  // namespace hkv
 

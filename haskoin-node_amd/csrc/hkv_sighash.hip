@@ -236,9 +236,10 @@ hipError_t launch_std_inputs(const uint8_t* txs, uint32_t n_tx, const uint32_t* 
 // ---------------------------------------------------------------------------
 namespace hkv {
 
-// per-input desc words and record offsets; counters[0] ends as the number of
-// candidate records | key-check records << 32 (the tail kernel reads it,
-// stream-ordered after the scan, and re-arms it)
+// per-input desc words and record offsets; *counters (the call's parity
+// word, zeroed by the call before) ends as the number of candidate records |
+// key-check records << 32 (the tail kernel reads it, stream-ordered after the
+// scan)
 hipError_t launch_ms_scan(const uint8_t* txs, uint32_t n_tx, const uint32_t* txt, const uint8_t* scripts,
                           uint32_t scripts_len, const hkv_input_job* jobs, uint32_t n, int32_t forkid,
                           uint32_t* desc, uint64_t* off, uint64_t* counters, hipStream_t st) {

@@ -248,24 +248,27 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * replayed on device (count == m and all keys valid).
  * ASYNCHRONOUS: everything is enqueued on hip_stream and the call returns
  * without waiting for any of it (the batch's multisig record count stays on
- * the device: one tail launch reads it and does nothing when it is 0), so a
+ * the device: the tail — inside the block kernel for a block-sized batch,
+ * else one launch after the verify — reads it and does nothing when it is
+ * 0), so a
  * caller may enqueue block k+1 while block k verifies, and hip_stream may be
  * gated on events recorded after the call. Batches run in chunks of 131,072
  * inputs (the multisig scratch is sized per chunk by its 16-of-16 bound, 136
  * candidate + 16 key-check records per input, allocated on first use).
  * Scratch footprint: (136 + 16) * 168 B per input of the largest chunk seen,
  * i.e. ~0.1 GB for a 4,000-input block, ~3.35 GB for a full 131,072 chunk.
- * A multisig tail whose grid barrier gave up leaves its multisig verdicts
- * at 0 and reports HKV_STATUS_TAIL_FAULT (below) — this form only through
- * hkv_device_fault; use the _status form to get it per call.
+ * A multisig tail whose work-queue wait gave up leaves its multisig
+ * verdicts at 0 and reports HKV_STATUS_TAIL_FAULT (below) — this form only
+ * through hkv_device_fault; use the _status form to get it per call.
  * n <= 0xFFFFFF00. */
 int hkv_verify_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv_input_job* d_jobs, size_t n,
                                  int32_t forkid, void* d_records, uint32_t* d_bits, void* hip_stream);
 /* Status bits a verify call reports (hkv_verify_std_inputs_device_status,
- * hkv_device_fault). HKV_STATUS_TAIL_FAULT: the multisig tail's grid barrier
- * gave up waiting (its workgroups were not co-resident — the tail is launched
- * cooperatively, so this should not happen): some multisig inputs of the
- * batch were left rejected whatever their signatures. Never a false accept. */
+ * hkv_device_fault). HKV_STATUS_TAIL_FAULT: a wait of the multisig tail's
+ * work queue gave up (seconds; the queue needs no co-residency, so only a
+ * hung or preempted workgroup, or the HKV_FAIL_TAIL test hook, causes it):
+ * some multisig inputs of the batch were left rejected whatever their
+ * signatures. Never a false accept. */
 #define HKV_STATUS_TAIL_FAULT 1u
 /* hkv_verify_std_inputs_device with a status word: d_status (device memory
  * of `dev`, or NULL) gets the call's HKV_STATUS_* bits ORed in on hip_stream,

@@ -65,19 +65,23 @@ def report(trace_dir: str, host_json: str) -> None:
     ks.sort()
     host = json.load(open(host_json))
     n = len(host["calls"])
-    # the last n (block kernel, tail kernel) pairs are the isolated calls
+    # the last n calls: (block kernel, tail kernel) pairs (or the block
+    # kernel alone, for a build that runs the tail inside it)
     pairs = []
     i = len(ks) - 1
-    while i > 0 and len(pairs) < n:
-        if "ms_tail" in ks[i][2] and "block_kernel" in ks[i - 1][2]:
+    while i >= 0 and len(pairs) < n:
+        if i > 0 and "ms_tail" in ks[i][2] and "block_kernel" in ks[i - 1][2]:
             pairs.append((ks[i - 1], ks[i]))
             i -= 2
+        elif "block_kernel" in ks[i][2]:
+            pairs.append((ks[i], ks[i]))
+            i -= 1
         else:
             i -= 1
     pairs.reverse()
     blk = [(b[1] - b[0]) / 1e3 for b, _ in pairs]
-    tail = [(t[1] - t[0]) / 1e3 for _, t in pairs]
-    gap = [(t[0] - b[1]) / 1e3 for b, t in pairs]
+    tail = [(t[1] - t[0]) / 1e3 for b, t in pairs if t is not b]
+    gap = [(t[0] - b[1]) / 1e3 for b, t in pairs if t is not b]
     span = [(t[1] - b[0]) / 1e3 for b, t in pairs]
     ev = [r["event_us"] for r in host["calls"]]
     enq = [r["enqueue_us"] for r in host["calls"]]
