@@ -453,7 +453,43 @@ def config0_block(v, torch, steps: int):
     res["workload"] = ("BASELINE configs[0]: 2,000 txs x 2 P2PKH inputs x 2 P2PKH outputs = 4,000 signatures, "
                        "seed 0x484B5631, compressed keys from a 4,096-key pool, SIGHASH_ALL, low S; "
                        "verifyStdInput semantics end to end on device")
+    res["native_caller"] = native_caller(txs, inputs)
     return res, recs, got, txs, inputs
+
+
+NATIVE = os.path.join(ROOT, "tools", "native_latency")
+
+
+def native_caller(txs, inputs, calls: int = 20) -> dict:
+    """The same block verified by a C++ caller through the C ABI only
+    (tools/native_latency.cpp, a child process: no Python or ctypes in front
+    of the call, as a Haskell node's FFI would call it): back to back, one
+    call alone, one call alone after 5 ms of GPU idle (HIP events)."""
+    import shutil
+    import subprocess
+    import tempfile
+    import numpy as np
+    from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
+    if not os.access(NATIVE, os.X_OK):
+        return {"skipped": "tools/native_latency not built (make -C haskoin-node_amd/csrc)"}
+    tb = TxBatch(txs)
+    jobs = np.zeros(len(inputs), dtype=INPUT_JOB_DTYPE)
+    for k, (t, i, spk, value) in enumerate(inputs):
+        off, ln = tb.script(spk)
+        jobs[k] = (t, i, off, ln, value)
+    _, pool = tb.struct()
+    d = tempfile.mkdtemp(prefix="hkv_blk_")
+    try:
+        for name, arr in (("txs", tb.bytes), ("offsets", tb.offsets), ("scripts", pool), ("jobs", jobs)):
+            np.ascontiguousarray(arr).tofile(os.path.join(d, name + ".bin"))
+        p = subprocess.run([NATIVE, d, str(calls)], capture_output=True, text=True, timeout=180)
+        if p.returncode != 0:
+            return {"error": f"exit {p.returncode}: {p.stderr.strip()[-300:]}"}
+        return json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 (reported in the line, never fatal to the bench)
+        return {"error": repr(e)[:300]}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def cpu_sighash_leg(txs, inputs, gpu_records) -> dict:
