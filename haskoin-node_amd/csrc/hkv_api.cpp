@@ -156,6 +156,9 @@ constexpr size_t STD_CHUNK = 1u << 17;
 constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
 constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFF00ull;
 constexpr size_t MS_BAR_WORDS = 32, MS_FAULT = 16, MS_HOST_STATUS = 17;  // DevCtx::ms_bar
+#ifndef HKV_TAIL_BLOCK_GRID
+#define HKV_TAIL_BLOCK_GRID 4096
+#endif
 
 int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
   if (d.im_cap < n_pad) {
@@ -634,7 +637,10 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
     if (rc) return rc;
   }
   // (operands taken after every launch before it has sized the scratch)
-  HKV_TRY(hkv::launch_ms_tail(tail_args(d, dt, jobs, n, forkid, out_bits, fused, ms, cap_cand), (uint32_t)d.n_cu, st),
+  // (a block-sized batch: a smaller tail grid, which a block without
+  // multisig inputs launches and retires sooner)
+  const uint32_t tail_grid = fused_scan ? std::min<uint32_t>((uint32_t)d.n_cu, HKV_TAIL_BLOCK_GRID) : (uint32_t)d.n_cu;
+  HKV_TRY(hkv::launch_ms_tail(tail_args(d, dt, jobs, n, forkid, out_bits, fused, ms, cap_cand), tail_grid, st),
           "multisig tail launch");
   ++d.tail_epoch;  // (launched: it zeroes the slot and the scan sum the next call uses)
   d.inject_tail = false;

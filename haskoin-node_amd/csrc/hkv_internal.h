@@ -77,7 +77,7 @@ struct MsTail {
   uint32_t* status;                 // the call's status word (HKV_STATUS_* ORed in), or null
   uint32_t force_fault;             // test hook (hkv_debug_fail_device HKV_FAIL_TAIL): every phase wait gives up
 };
-hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st);
+hipError_t launch_ms_tail(const MsTail& a, uint32_t grid, hipStream_t st);  // grid <= n_cu (its scratch slots)
 uint32_t ms_tail_slots(uint32_t n_cu);  // signatures in flight (im / aux slots the tail needs)
 // small batches of standard inputs in one launch; with ms, the block kernel
 // (std_split_scans) also runs the multisig scan; with tx_off (the block

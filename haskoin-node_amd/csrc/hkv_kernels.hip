@@ -2682,8 +2682,8 @@ hipError_t launch_std_verify_split(const uint8_t* txs, uint32_t n_tx, const uint
   return hipGetLastError();
 }
 uint32_t ms_tail_slots(uint32_t n_cu) { return n_cu * PAIR_SIGS; }
-hipError_t launch_ms_tail(const MsTail& a, uint32_t n_cu, hipStream_t st) {
-  hipLaunchKernelGGL(hkv_ms_tail_kernel, dim3(n_cu), dim3(PAIR_TPB), 0, st, a);
+hipError_t launch_ms_tail(const MsTail& a, uint32_t grid, hipStream_t st) {
+  hipLaunchKernelGGL(hkv_ms_tail_kernel, dim3(grid), dim3(PAIR_TPB), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_gtable(uint32_t* gtab, hipStream_t st) {
