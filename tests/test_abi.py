@@ -66,3 +66,22 @@ def test_kernel_code_object_is_gfx950():
     blob = open(LIB, "rb").read()
     assert b"gfx950" in blob
     assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_native_caller_builds_and_links_only_the_c_abi():
+    """tools/native_latency (bench.py config0.native_caller) is built with the
+    library and calls it through include/hkv.h alone: it links libhkv.so from
+    the tree (rpath) and imports only hkv_* symbols from it; without a block
+    directory it prints its usage and exits 2 before touching a device."""
+    tool = os.path.join(ROOT, "tools", "native_latency")
+    if not os.path.exists(tool):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "haskoin-node_amd", "csrc")], check=True,
+                       stdout=subprocess.DEVNULL)
+    ldd = subprocess.run(["ldd", tool], capture_output=True, text=True, check=True).stdout
+    assert os.path.realpath(LIB) in {os.path.realpath(l.split("=>")[1].split("(")[0].strip())
+                                     for l in ldd.splitlines() if "libhkv.so" in l}
+    nm = subprocess.run(["nm", "-D", "--undefined-only", tool], capture_output=True, text=True, check=True).stdout
+    used = sorted({l.split()[-1] for l in nm.splitlines() if l.split() and l.split()[-1].startswith("hkv_")})
+    assert used and set(used) <= set(header_functions()), used
+    p = subprocess.run([tool], capture_output=True, text=True)
+    assert p.returncode == 2 and "usage" in p.stderr
