@@ -6,6 +6,7 @@ calls below really overlap in libhkv: host-form and device-form entry
 points, record batches and standard-input blocks with multisig inputs (whose
 scan sums and tail queue slots alternate per call), each device-form caller
 on its own stream. Every call must return its own batch's verdicts."""
+import os
 import random
 import threading
 
@@ -54,7 +55,7 @@ def _bits(torch, w, n):
 
 def test_threads_share_one_context(torch, ver, coracle):
     import hkv
-    rounds = 4
+    rounds = int(os.environ.get("HKV_STRESS_ROUNDS", "4"))  # (a longer stress run: HKV_STRESS_ROUNDS=40)
     # record batches: generated valid records, every third one's r corrupted
     n = 70_000
     d_a = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
@@ -145,7 +146,7 @@ def test_threads_share_one_context(torch, ver, coracle):
     for t in threads:
         t.start()
     for t in threads:
-        t.join(timeout=90)
+        t.join(timeout=max(90, 20 * rounds))
     assert not any(t.is_alive() for t in threads), "a caller did not return (deadlock?)"
     assert not errors, errors
     assert sorted(done) == sorted(name for name, _ in callers)
