@@ -919,13 +919,19 @@ def test_block_kernel_random_wire_mutations_vs_oracle(torch, ver, coracle):
     (a tx that no longer parses rejects) and every record the block kernel
     wrote equals the oracle's. Complements the structured malformed-wire
     cases with positions the structure does not pick."""
+    _wire_mutation_batch(torch, ver, coracle, 0xF022)
+
+
+def _wire_mutation_batch(torch, ver, coracle, seed, n_mut=1500):
+    """One block-sized batch of n_mut random wire mutants (seeded) beside
+    their originals: GPU verdicts and records == the oracle's, both forms."""
     import hkv
-    rng = random.Random(0xF022)
+    rng = random.Random(seed)
     keys = [txgen.Key(rng.randrange(1, o.N), compressed=(k % 4 != 0)) for k in range(8)]
     txs, jobs = txgen.std_block(rng, 120, keys, p2wpkh_share=0.4, p2pk_share=0.2, p2sh_share=0.2)
     raw = [sh.tx_serialize(t) for t in txs]
     all_raw, all_jobs, kinds = list(raw), list(jobs), ["valid"] * len(jobs)
-    for _ in range(1500):
+    for _ in range(n_mut):
         t, i, p, v = rng.choice(jobs)
         b = bytearray(raw[t])
         k = rng.randrange(6)
@@ -966,3 +972,13 @@ def test_block_kernel_random_wire_mutations_vs_oracle(torch, ver, coracle):
     badr = [kinds[k] for k in range(len(all_jobs)) if recs[k * 168:(k + 1) * 168] != exp[k]]
     assert not badr, badr[:10]
     assert hkv.verify_std_inputs(ver, all_raw, all_jobs) == want
+
+
+@pytest.mark.skipif(not os.environ.get("HKV_STRESS_SEEDS"), reason="stress run only (HKV_STRESS_SEEDS=n)")
+def test_block_kernel_wire_mutation_stress(torch, ver, coracle):
+    """The mutation batch above over HKV_STRESS_SEEDS further seeds (a stress
+    run outside the suite: profiles/r05o/)."""
+    for k in range(int(os.environ["HKV_STRESS_SEEDS"])):
+        _wire_mutation_batch(torch, ver, coracle, 0x5EED0000 + k)
+        if k % 20 == 19:
+            print(f"wire mutation stress: {k + 1} batches ({(k + 1) * 1500} mutants) match", flush=True)
