@@ -2,6 +2,7 @@
 oracle — bit-exact verdicts, both modes, golden KATs, random and adversarial
 batches, field/scalar known answers, determinism, the 1M-record size."""
 import ctypes
+import os
 import random
 
 import numpy as np
@@ -534,3 +535,30 @@ def test_multi_device_failover_reshards(torch, ver):
         assert (got == single).all()
         assert [lib.hkv_device_failures(v3.ctx, k) for k in range(3)] == [1, 1, 1]
     assert not single[bad].any() and single.sum() == n - bad.size
+
+
+@pytest.mark.skipif(not os.environ.get("HKV_STRESS_RECORD_BATCHES"),
+                    reason="stress run only (HKV_STRESS_RECORD_BATCHES=n)")
+def test_record_byte_mutation_stress(torch, ver, coracle):
+    """Opt-in stress (profiles/r05p/): n batches of 262,144 generated records
+    with 30 % of them damaged at one random byte (any of the 168: msg32, r,
+    s, the key's length byte, prefix or coordinates, the padding) to a random
+    value; the verdicts of both modes, at the full-grid launch shape, equal
+    the C restatement's on every record."""
+    n = 262144
+    for k in range(int(os.environ["HKV_STRESS_RECORD_BATCHES"])):
+        d = gen_device(torch, ver, n, seed=0x53545200 + k, unc=200)
+        host = d.cpu().numpy().copy().reshape(-1, 168)
+        rng = np.random.default_rng(0x5EED + k)
+        hit = rng.random(n) < 0.3
+        rows = np.nonzero(hit)[0]
+        cols = rng.integers(0, 168, size=rows.size)
+        host[rows, cols] = rng.integers(0, 256, size=rows.size, dtype=np.uint8)
+        flat = host.reshape(-1)
+        for mode in (0, 1):
+            exp = oracle_batch(coracle, flat.tobytes(), mode, threads=host_threads())
+            got = ver.verify_records(flat, mode)
+            mism = np.nonzero(got != exp)[0]
+            assert mism.size == 0, (k, mode, mism[:10], [int(c) for c in cols[np.isin(rows, mism[:10])]])
+        print(f"record mutation stress: batch {k + 1}: {rows.size} damaged of {n}, accepts {int(got.sum())}",
+              flush=True)
