@@ -982,3 +982,25 @@ def test_block_kernel_wire_mutation_stress(torch, ver, coracle):
         _wire_mutation_batch(torch, ver, coracle, 0x5EED0000 + k)
         if k % 20 == 19:
             print(f"wire mutation stress: {k + 1} batches ({(k + 1) * 1500} mutants) match", flush=True)
+
+
+@pytest.mark.skipif(not os.environ.get("HKV_STRESS_MS_BLOCKS"), reason="stress run only (HKV_STRESS_MS_BLOCKS=n)")
+def test_multisig_block_stress(torch, ver, coracle):
+    """Opt-in stress (profiles/r05q/): n seeded block-kernel batches, each a
+    coinbase no input spends, signed single-signature inputs and every
+    multisig case of txgen (bare / P2SH / P2WSH / P2SH-P2WSH, m-of-n, wrong
+    order, bad keys, NULLDUMMY), fork id alternating: device-form verdicts
+    (and every fifth batch the host form) equal the oracle's on every input,
+    and no call reports a tail fault."""
+    import hkv
+    for k in range(int(os.environ["HKV_STRESS_MS_BLOCKS"])):
+        forkid = None if k % 2 == 0 else 0
+        raw, jobs, labels = _ms_block(random.Random(0x4D530000 + k), forkid)
+        want = _ms_oracle(coracle, raw, jobs, forkid)
+        got, st = _device_verify_std(torch, ver, raw, jobs, forkid, status=True)
+        bad = [(labels[j], got[j], want[j]) for j in range(len(jobs)) if got[j] != want[j]]
+        assert not bad and st == 0, (k, st, bad[:10])
+        if k % 5 == 0:
+            assert hkv.verify_std_inputs(ver, raw, jobs, forkid) == want, k
+        print(f"multisig block stress: {k + 1} batches ({len(jobs)} inputs) match", flush=True)
+    assert ver.device_fault(0) == 0
