@@ -409,7 +409,15 @@ HKV_DEV uint32_t late_u1_lane(const uint32_t* __restrict__ recs, uint32_t i, uin
 // caller's validity so far (updated); sinv is s^-1 (of 1 when !ok) for the u1
 // half (sig_lane_g).
 HKV_DEV void sig_lane_q(sc r, sc s, uint32_t mode, uint32_t* __restrict__ im, uint32_t n_pad, uint32_t i, bool& ok,
-                        bool& glv_ok, bool& n1, bool& n2, sc& sinv) {
+                        bool& glv_ok, bool& n1, bool& n2, sc& sinv, unsigned long long* sclk = nullptr) {
+#if HKV_SIG_STAMPS == 4  // measurement builds only: s^-1 and the GLV split of workgroup 0's signature wave
+  auto qmark = [&](int slot) {
+    if (sclk != nullptr && (threadIdx.x & 63) == 0) sclk[4 + slot] = wall_clock64();
+  };
+#else
+  auto qmark = [&](int) {};
+  (void)sclk;
+#endif
   ok = ok && u256_lt(r.v, SC_N) && u256_lt(s.v, SC_N);
   const bool high = sc_is_high(s);
   if (mode == HKV_MODE_HASKOIN) {
@@ -423,9 +431,11 @@ HKV_DEV void sig_lane_q(sc r, sc s, uint32_t mode, uint32_t* __restrict__ im, ui
   if (!ok) sc_set_u32(s, 1);
   sc u2;
   sc_inv(sinv, s);
+  qmark(9);  // (HKV_SIG_STAMPS 4: "hi_table" = s^-1 done)
   sc_mul(u2, r, sinv);
   uint32_t k1[5], k2[5];
   glv_ok = glv_split(u2, k1, n1, k2, n2);
+  qmark(2);  // (HKV_SIG_STAMPS 4: "digits" = u2 and the GLV split done)
   const bool use = ok && glv_ok;
   uint32_t S1[5], S2[5];
 #pragma unroll
@@ -927,13 +937,12 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
                             const uint32_t* __restrict__ recs, const StdArgs& sa, StdIn& x, sc& m, sc& sinv,
                             bool& use, uint32_t& flags, TxView v = {nullptr, nullptr},
                             unsigned long long* sclk = nullptr) {
-#if HKV_SIG_STAMPS == 2
+#if HKV_SIG_STAMPS == 2 || HKV_SIG_STAMPS == 4
   auto smark = [&](int slot) {
     if (sclk != nullptr && (threadIdx.x & 63) == 0) sclk[4 + slot] = wall_clock64();
   };
 #else
   auto smark = [&](int) {};
-  (void)sclk;
 #endif
   flags = 0;
   use = false;
@@ -955,7 +964,7 @@ HKV_DEV void sig_wave_parse(uint32_t i, bool on, uint32_t n, uint32_t n_pad, uin
     rec_be256(s.v, w, 64);
     rec_be256(m.v, w, 0);
   }
-  sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv);
+  sig_lane_q(r, s, mode, im, n_pad, i, ok, glv_ok, n1, n2, sinv, sclk);
   smark(8);
   use = ok && glv_ok;
   fe kx, kwv;
@@ -1480,6 +1489,9 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
   auto mark = [&](int slot) {
 #if HKV_SIG_STAMPS
     if (slot == STAMP_TABLE0 || slot == STAMP_P || slot == STAMP_SQRT) return;  // the signature wave's
+#endif
+#if HKV_SIG_STAMPS == 4
+    if (slot == STAMP_TABLE1) return;
 #endif
     if (stamp) clk[4 + slot] = wall_clock64();
   };
