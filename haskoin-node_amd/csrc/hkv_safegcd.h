@@ -35,6 +35,10 @@
 #ifndef HKV_SGCD_EARLY
 #define HKV_SGCD_EARLY 1
 #endif
+// HKV_SGCD_FLAT: the device's divstep loop without branches (divsteps30)
+#ifndef HKV_SGCD_FLAT
+#define HKV_SGCD_FLAT 1
+#endif
 #if defined(__HIPCC__)
 #define HKV_HD __host__ __device__ __forceinline__
 #else
@@ -83,6 +87,45 @@ HKV_HD int ctz32(uint32_t x) { return __builtin_ctz(x); }  // x != 0
 HKV_HD int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
   int i = 30;
+#if (defined(__HIP_DEVICE_COMPILE__) && HKV_SGCD_FLAT) || defined(HKV_SGCD_FLAT_HOST)
+  // Branch-free on the device (HKV_SGCD_FLAT_HOST: the same form in the host
+  // test build, one lane): the lanes of a wave run different numbers of
+  // iterations, so each step is written with selects and a lane that is done
+  // (i = 0) steps with zeros = 0 and w = 0, which changes nothing; the loop
+  // ends once no lane has steps left. The branchy form spends each iteration
+  // on exec-mask bookkeeping for the swap and the exit.
+  for (;;) {
+    const int zeros = ctz32(g | (0xFFFFFFFFu << i));  // i = 0: all ones, zeros = 0
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!__any(i != 0)) break;
+#else
+    if (i == 0) break;
+#endif
+    const bool live = i != 0;
+    const bool sw = live && eta < 0;  // g odd and delta > 0: (f, g, u, v, q, r) <- (g, -f, q, r, -u, -v)
+    const uint32_t f0 = f, u0 = u, v0 = v;
+    f = sw ? g : f;
+    g = sw ? 0u - f0 : g;
+    u = sw ? q : u;
+    q = sw ? 0u - u0 : q;
+    v = sw ? r : v;
+    r = sw ? 0u - v0 : r;
+    eta = sw ? -eta : eta;
+    const int limit = (eta + 1) > i ? i : (eta + 1);
+    const uint32_t m = live ? ((0xFFFFFFFFu >> (32 - limit)) & 255u) : 0u;
+    uint32_t x = (3u * f) ^ 2u;  // f^-1 mod 2^5 (f odd)
+    x *= 2u - f * x;             // mod 2^10
+    const uint32_t w = (0u - g * x) & m;
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+#else
   for (;;) {
     const int zeros = ctz32(g | (0xFFFFFFFFu << i));  // the sentinel bit i stops the count
     g >>= zeros;
@@ -107,6 +150,7 @@ HKV_HD int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
     q += u * w;
     r += v * w;
   }
+#endif
   t[0] = (int32_t)u;
   t[1] = (int32_t)v;
   t[2] = (int32_t)q;

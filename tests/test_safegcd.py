@@ -82,3 +82,23 @@ def test_safegcd_full_bound_equals_early_stop(binary, binary_full):
     assert run(binary, xs) == run(binary_full, xs) == [pow(x, -1, N) for x in xs]
     ps = [1, P - 1] + [rng.randrange(1, P) for _ in range(3000)]
     assert run(binary, ps, "p") == run(binary_full, ps, "p") == [pow(x, -1, P) for x in ps]
+
+
+@pytest.fixture(scope="module")
+def binary_flat(tmp_path_factory):
+    """The device's branch-free divstep loop (HKV_SGCD_FLAT) built for the host."""
+    return build(tmp_path_factory, "safegcd_host_flat", "-DHKV_SGCD_FLAT_HOST")
+
+
+def test_safegcd_flat_loop_equals_branchy(binary, binary_flat):
+    """The branch-free divsteps (the kernels' form) give the same inverses as
+    the branchy form on edge and random scalars, mod n and mod p."""
+    rng = random.Random(0x5F1A7)
+    vals = [1, 2, 3, N - 1, N - 2, (N + 1) // 2, 1 << 128, (1 << 255) % N] + [rng.randrange(1, N) for _ in range(3000)]
+    P = (1 << 256) - (1 << 32) - 977
+    pv = [1, 2, P - 1, (1 << 200) + 7] + [rng.randrange(1, P) for _ in range(2000)]
+    for mod, xs, m in (("n", vals, N), ("p", pv, P)):
+        a, b = run(binary, xs, mod), run(binary_flat, xs, mod)
+        assert a == b
+        assert all(x * y % m == 1 for x, y in zip(xs, b))
+
