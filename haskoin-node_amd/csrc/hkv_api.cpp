@@ -867,11 +867,19 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
     else d.hbits_cap = words;
   }
   if (rc) return rc;
+  // Chunk schedule: the first chunk is one resident grid (its H2D is the only
+  // copy no verify hides), each next one twice the one before (PCIe moves
+  // ~2.8x the records per second the verify does, so the copy of chunk c+1
+  // still ends before the verify of chunk c), in whole grids; a remainder
+  // under one grid joins the chunk before it. (One quarter of the shard per
+  // chunk exposed a quarter-shard H2D before the first verify.)
   const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
-  const size_t chunk = len >= 2 * grid_lanes ? grid_lanes * std::max<size_t>(1, (len / 4) / grid_lanes) : len;
   const uint8_t* src = host + s.lo * hkv::REC_SIZE;
-  for (size_t off = 0; off < len && !rc; off += chunk) {
-    const size_t cl = std::min(chunk, len - off);
+  size_t next = len >= 2 * grid_lanes ? grid_lanes : len;
+  for (size_t off = 0, cl = 0; off < len && !rc; off += cl) {
+    cl = std::min(next, len - off);
+    if (len - off - cl < grid_lanes) cl = len - off;
+    next = std::min(2 * next, (size_t)1 << 40);
     hipEvent_t ev = nullptr;
     hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) {
