@@ -156,6 +156,9 @@ constexpr size_t STD_CHUNK = 1u << 17;
 constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
 constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFF00ull;
 constexpr size_t MS_BAR_WORDS = 32, MS_FAULT = 16, MS_HOST_STATUS = 17;  // DevCtx::ms_bar
+#ifndef HKV_HOST_FIRST_DIV  // the host-batch path's first chunk: one resident grid / this
+#define HKV_HOST_FIRST_DIV 4
+#endif
 #ifndef HKV_TAIL_BLOCK_GRID
 #define HKV_TAIL_BLOCK_GRID 4096
 #endif
@@ -867,19 +870,22 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
     else d.hbits_cap = words;
   }
   if (rc) return rc;
-  // Chunk schedule: the first chunk is one resident grid (its H2D is the only
-  // copy no verify hides), each next one twice the one before (PCIe moves
-  // ~2.8x the records per second the verify does, so the copy of chunk c+1
-  // still ends before the verify of chunk c), in whole grids; a remainder
-  // under one grid joins the chunk before it. (One quarter of the shard per
-  // chunk exposed a quarter-shard H2D before the first verify.)
+  // Chunk schedule: the first chunk is a quarter of a resident grid (its H2D
+  // is the only copy no verify hides), then one grid, then each chunk twice
+  // the one before (PCIe moves ~2.8x the records per second the verify does,
+  // so the copy of chunk c+1 still ends before the verify of chunk c), in
+  // whole grids; a remainder under one grid joins the chunk before it.
+  // (Same-box A/B, profiles/r05z/: 1M records 9.84 / 9.97 ms against 10.58
+  // with a one-grid first chunk and 10.75 / 10.69 with an eighth; one
+  // quarter of the shard per chunk, the earlier schedule, exposed a
+  // quarter-shard H2D before the first verify: 16M 161 ms, now 146 ms.)
   const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
   const uint8_t* src = host + s.lo * hkv::REC_SIZE;
-  size_t next = len >= 2 * grid_lanes ? grid_lanes : len;
+  size_t next = len >= 2 * grid_lanes ? grid_lanes / HKV_HOST_FIRST_DIV : len;
   for (size_t off = 0, cl = 0; off < len && !rc; off += cl) {
     cl = std::min(next, len - off);
     if (len - off - cl < grid_lanes) cl = len - off;
-    next = std::min(2 * next, (size_t)1 << 40);
+    next = std::min(std::max(2 * next, grid_lanes), (size_t)1 << 40);
     hipEvent_t ev = nullptr;
     hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) {
