@@ -58,6 +58,9 @@ __constant__ static const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC
 // ---------------------------------------------------------------------------
 // 1. prologue
 // ---------------------------------------------------------------------------
+#ifndef HKV_TOP_MERGE  // 1: a chain from the top window takes the top two windows as one digit (pair_chain)
+#define HKV_TOP_MERGE 1
+#endif
 #ifndef HKV_PROLOGUE_WAVES
 #define HKV_PROLOGUE_WAVES 4  // min waves per SIMD the prologue's register allocation targets
 #endif
@@ -635,27 +638,53 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
     fe_set_zero(acc.y);
     fe_set_zero(acc.z);
     uint32_t dw = valid ? im[(size_t)(IM_DIG + NWIN - 1) * n_pad + i] : DIG_ZERO;
+    int win = NWIN - 1;
+    bool dbl = false;       // the first window starts from infinity: no doublings
+    int x1 = 0, x2 = 0;     // the merged top window's second terms (pair_chain)
+    int nterm = 2;          // Q terms of the current window
+#if HKV_TOP_MERGE
+    {
+      // the top two windows as one digit in [0, 16] per half, taken as
+      // min(m, 8) + (m - 8)+ (pair_chain): two additions where every wave
+      // ran the second window's 4 doublings (5 % of the halves reach 2^127)
+      const uint32_t dw2 = valid ? im[(size_t)(IM_DIG + NWIN - 2) * n_pad + i] : DIG_ZERO;
+      const int t1 = (((int)(dw & QDIG_MASK) - QBIAS) << QW) + (int)(dw2 & QDIG_MASK) - QBIAS;
+      const int t2 = (((int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS) << QW) + (int)((dw2 >> QDIG_BITS) & QDIG_MASK) - QBIAS;
+      if (!__any(t1 < 0 || t1 > 2 * QBIAS || t2 < 0 || t2 > 2 * QBIAS)) {
+        const int e1 = t1 < QBIAS ? t1 : QBIAS, e2 = t2 < QBIAS ? t2 : QBIAS;
+        x1 = t1 - e1;
+        x2 = t2 - e2;
+        dw = (uint32_t)(e1 + QBIAS) | ((uint32_t)(e2 + QBIAS) << QDIG_BITS);
+        win = NWIN - 2;
+        nterm = 4;
+      }
+    }
+#endif
 #pragma unroll 1
-    for (int win = NWIN - 1; win >= 0; --win) {
+    for (; win >= 0; --win) {
       const int d1 = (int)(dw & QDIG_MASK) - QBIAS, d2 = (int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS;
-      const int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
-      const int i1 = m1 ? m1 - 1 : 0, i2 = m2 ? m2 - 1 : 0;
       const uint32_t dw_next = (win > 0 && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
-      if (win != NWIN - 1) {
+      if (dbl) {
 #pragma unroll 1
         for (int d = 0; d < QW; ++d) {
           if (!inf) ec_double<ILP>(acc);
         }
       }
-      // Q terms: slot 0 = k1 * Q', slot 1 = k2 * lambda(Q')
+      dbl = true;
+      // Q terms: slot 0 = k1 * Q', slot 1 = k2 * lambda(Q') (terms 2, 3: the
+      // merged top window's second terms, run only when a lane of the wave has one)
 #pragma unroll 1
-      for (int slot = 0; slot < 2; ++slot) {
-        const int dg = slot == 0 ? d1 : d2;
+      for (int t = 0; t < nterm; ++t) {
+        const int slot = t & 1;
+        const int dg = t < 2 ? (slot == 0 ? d1 : d2) : (slot == 0 ? x1 : x2);
         const bool take = dg != 0;
+        if (t >= 2 && !__any(take)) continue;
+        const int mg = dg < 0 ? -dg : dg;
+        const int ie = mg ? mg - 1 : 0;
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
         fe tx, ty;
-        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), (slot == 0 ? 0 : 4), tx);
-        qtab_load(qs, n_lanes, lane, (slot == 0 ? i1 : i2), 2, ty);
+        qtab_load(qs, n_lanes, lane, ie, (slot == 0 ? 0 : 4), tx);
+        qtab_load(qs, n_lanes, lane, ie, 2, ty);
         fe_cneg(ty, ty, neg);
         const bool was_inf = inf;
         ec_accumulate<ILP>(acc, inf, acc.z, tx, ty, take);
@@ -663,6 +692,7 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
         // the 24 selects in every window where no lane of the wave does
         if (__any(take && was_inf)) gej_accumulate_from_inf(acc, inf, tx, ty, take && was_inf);
       }
+      nterm = 2;
       dw = dw_next;
     }
 
@@ -832,19 +862,53 @@ HKV_DEV void pair_chain(fe& P, fe& Z, bool& inf, const QLane& ql, const uint32_t
   inf = true;
   fe_set_zero(P);
   fe_set_zero(Z);
+  auto digit = [&](uint32_t w) { return half ? (int)((w >> QDIG_BITS) & QDIG_MASK) - QBIAS : (int)(w & QDIG_MASK) - QBIAS; };
   uint32_t dw = valid ? im[(size_t)(IM_DIG + w_hi) * n_pad + i] : DIG_ZERO;
+  bool dbl = false;  // the first window starts from infinity: no doublings
+#if HKV_TOP_MERGE
+  if (w_hi == NWIN - 1 && w_hi > w_lo) {
+    // The top two windows as one digit m = 2^QW d_top + d_next. The GLV
+    // halves are < 2^128 in practice (the bound the device split asserts is
+    // 2^129), so d_top is bit 127 and m is the unsigned value of bits
+    // 124..127 plus bit 123, in [0, 16]: taken as min(m, 8) + (m - 8)+ from
+    // the 8-entry table, one addition at most, where a top digit of 1 on any
+    // pair of the wave made every pair run the next window's 4 doublings (5 %
+    // of the halves reach 2^127: 80 % of the block kernel's groups). A wave
+    // with any m outside [0, 16] runs the windows one by one.
+    const uint32_t dw2 = valid ? im[(size_t)(IM_DIG + w_hi - 1) * n_pad + i] : DIG_ZERO;
+    const int m = (digit(dw) << QW) + digit(dw2);
+    if (!__any(m < 0 || m > 2 * QBIAS)) {
+      const int e1 = m < QBIAS ? m : QBIAS, e2 = m - e1;
+      fe T;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) T.v[k] = ql[e1 ? e1 - 1 : 0][k][ln];
+      fe_cneg(T, T, negh && odd);
+      pair_accumulate_from_inf(P, Z, inf, T, e1 != 0);
+      if (__any(e2 != 0)) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) T.v[k] = ql[e2 ? e2 - 1 : 0][k][ln];
+        fe_cneg(T, T, negh && odd);
+        pair_accumulate(P, Z, inf, T, e2 != 0, odd);  // T[8] + T[8] (m = 16): its exact doubling
+      }
+      w_hi -= 2;
+      dbl = true;
+      dw = (w_hi >= w_lo && valid) ? im[(size_t)(IM_DIG + w_hi) * n_pad + i] : DIG_ZERO;
+    }
+  }
+#endif
 #pragma unroll 1
   for (int win = w_hi; win >= w_lo; --win) {
-    const int dg = half ? (int)((dw >> QDIG_BITS) & QDIG_MASK) - QBIAS : (int)(dw & QDIG_MASK) - QBIAS;
+    const int dg = digit(dw);
     const int mg = dg < 0 ? -dg : dg;
     const int ie = mg ? mg - 1 : 0;
     const uint32_t dw_next = (win > w_lo && valid) ? im[(size_t)(IM_DIG + win - 1) * n_pad + i] : DIG_ZERO;
-    if (win != w_hi) {
+    if (dbl) {
 #pragma unroll 1
       for (int d = 0; d < QW; ++d) {
         if (!inf) pair_double(P, Z, odd);
       }
     }
+    dbl = true;
     const bool take = dg != 0;
     const bool neg = (dg < 0) != negh;
     fe T;

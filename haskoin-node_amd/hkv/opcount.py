@@ -30,7 +30,7 @@ QW = 4               # Booth radix 2^QW of the k1 / k2 windows (hkv_layout.h HKV
 Q_WINDOWS = (130 + QW - 1) // QW     # 26 (radix 32) / 33 (radix 16)
 Q_TABLE = 1 << (QW - 1)              # j*Q, j = 1..16 (radix 32) / 1..8
 G_WINDOWS = 7        # radix-2^20 Booth over 140 bits (u1 halves)
-DOUBLINGS = QW * (Q_WINDOWS - 1)
+DOUBLINGS = QW * (Q_WINDOWS - 2)   # the top two windows merged (HKV_TOP_MERGE)
 
 SC_INV_LOW = 0x0BAAEDCE6AF48A03BBFD25E8CD036413F
 BATCH_INV = 16       # signatures per s^-1 (hkv_layout.h)
@@ -47,7 +47,10 @@ def ecmult_products(qw: int = QW, beta_per_lookup: bool = False) -> int:
     form beta * x per addition instead of storing it."""
     q_table = 1 << (qw - 1)
     q_windows = (130 + qw - 1) // qw
-    doublings = qw * (q_windows - 1)
+    # radix 16: the top two windows run as one (HKV_TOP_MERGE: the halves are
+    # < 2^128), their up to four additions counted as the two windows' two
+    # each; radix 32's top window already holds bits 125..127 (no merge)
+    doublings = qw * (q_windows - (2 if qw == 4 else 1))
     beta_t = 0 if beta_per_lookup else 1             # beta * x per table entry, or per lambda addition
     table = (GEJ_DOUBLE                      # 2Q
              + FE_SQR + 3 * FE_MUL           # Q' = (x Z^2, y Z^3)

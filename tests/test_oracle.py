@@ -59,6 +59,37 @@ def booth(k, w, nwin):
     return digits
 
 
+def test_top_window_merge_digit_range():
+    """HKV_TOP_MERGE (pair_chain, hkv_ecmult_kernel): the top two radix-16
+    windows of a GLV half run as one digit m = 16 d32 + d31, taken from the
+    8-entry table as min(m, 8) + (m - 8)+. That needs m in [0, 16] for every
+    half: the rounding split bounds |k1| by (|a1| + |a2|) / 2 and |k2| by
+    (|b1| + |b2|) / 2, both < 2^128 (a wave with any m outside the range
+    would run the windows one by one)."""
+    assert (abs(o.A1) + abs(o.A2)) // 2 < 2**128 and (abs(o.B1) + abs(o.B2)) // 2 < 2**128
+    rng = random.Random(11)
+    g1 = (2**384 * o.B2 + o.N // 2) // o.N
+    g2 = (2**384 * (-o.B1) + o.N // 2) // o.N
+    ks = [rng.randrange(o.N) for _ in range(3000)] + [0, 1, o.N - 1, o.LAMBDA, 2**128, 2**255, o.N // 2]
+    seen_top = 0
+    for k in ks:
+        c1 = (k * g1 + 2**383) >> 384
+        c2 = (k * g2 + 2**383) >> 384
+        k2 = (c1 * (-o.B1) + c2 * (-o.B2)) % o.N
+        k1 = (k - k2 * o.LAMBDA) % o.N
+        for kk in (k1, k2):
+            mag = o.N - kk if kk > o.N // 2 else kk
+            assert mag < 2**128
+            d = booth(mag, 4, 33)
+            m = 16 * d[32] + d[31]
+            assert 0 <= m <= 16
+            e1 = min(m, 8)
+            assert 0 <= m - e1 <= 8
+            assert (e1 + (m - e1)) * 16**31 + sum(x * 16**i for i, x in enumerate(d[:31])) == mag
+            seen_top += d[32] != 0
+    assert seen_top > 0  # the case the merge removes a window of doublings for
+
+
 def test_booth_recoding_identity():
     """Booth digits as the ecmult kernel extracts them: radix 16 (Q windows,
     the default hkv_layout.h HKV_QW = 4: 33 windows of -8..8), radix 32 (the

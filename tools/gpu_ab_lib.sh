@@ -20,6 +20,6 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 b = d["block_mix"]
 print(sys.argv[1], "config0_us", d["config0"]["total_us"], "block_us", b["block"]["total_us"],
-      "batch32_us", b["batch32"]["total_us"], "value", round(d["value"] / 1e6, 2), "sclk", d["roofline"].get("sclk_mhz"))
+      "pool16k_us", b["pool16k"]["total_us"], "batch32_us", b["batch32"]["total_us"], "value", round(d["value"] / 1e6, 2), "sclk", d["roofline"].get("sclk_mhz"))
 PY
 done
