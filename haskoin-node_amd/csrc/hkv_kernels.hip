@@ -1353,7 +1353,11 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
 #ifndef HKV_BLK_K2
 #define HKV_BLK_K2 27
 #endif
+#ifndef HKV_BLK_K1_HASHED  // the lo / mid split of a group with BIP143 per-tx hashes on wave 0 (0: BLK_K1)
+#define HKV_BLK_K1_HASHED 0
+#endif
 constexpr int BLK_K1 = HKV_BLK_K1, BLK_K2 = HKV_BLK_K2;
+static_assert(HKV_BLK_K1_HASHED == 0 || (HKV_BLK_K1_HASHED >= 2 && HKV_BLK_K1_HASHED < HKV_BLK_K2), "three segments");
 static_assert(BLK_K1 >= 2 && BLK_K1 < BLK_K2 && BLK_K2 <= NWIN - 1, "three non-empty segments");
 constexpr int BLK_SIGS = 16;
 constexpr int BLK_TPB = 256;
@@ -1463,19 +1467,21 @@ HKV_DEV TxView blk_view(const C& tc, uint32_t c) {
 // by its record). Every input whose tx carries a witness section, or every
 // input on a fork-id network, gets them; the sighash uses them only for the
 // BIP143 form, which needs a witness tx (or FORKID).
+// input i's tx needs the BIP143 per-tx hashes (row: its index row)
+HKV_DEV bool blk_needs_tx_hashes(const StdArgs& sa, uint32_t i, uint32_t n, const uint32_t*& row) {
+  row = sa.txt;
+  if (i >= n) return false;
+  const hkv_input_job jb = sa.jobs[i];
+  if (jb.tx >= sa.n_tx) return false;
+  row = sa.txt + (size_t)jb.tx * TXT_WORDS;
+  const uint32_t f = row[TXT_FLAGS];
+  return (f & TXF_OK) && ((f & TXF_WITNESS) || sa.forkid >= 0);
+}
 HKV_DEV void blk_tx_hashes(const StdArgs& sa, const TxCache& tc, uint32_t base, uint32_t n, uint32_t* recs,
                            uint32_t* shabuf) {
   const uint32_t c = (threadIdx.x & 63u) & (BLK_SIGS - 1), i = base + c;
-  const uint32_t* row = sa.txt;
-  bool need = false;
-  if (i < n) {
-    const hkv_input_job jb = sa.jobs[i];
-    if (jb.tx < sa.n_tx) {
-      row = sa.txt + (size_t)jb.tx * TXT_WORDS;
-      const uint32_t f = row[TXT_FLAGS];
-      need = (f & TXF_OK) && ((f & TXF_WITNESS) || sa.forkid >= 0);
-    }
-  }
+  const uint32_t* row;
+  const bool need = blk_needs_tx_hashes(sa, i, n, row);
   bip143_tx_hashes_spread(sa.txs, row, need, recs + (size_t)(i < n ? i : 0u) * REC_WORDS + 8, shabuf, BLK_SIGS,
                           txc_view(tc, c).t);
 }
@@ -1603,6 +1609,16 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     // 244.6 us, configs[2] 248.7 -> 246.6 / 247.3 us, profiles/r04r_prio/)
     __builtin_amdgcn_s_setprio(HKV_CHAIN_PRIO);
 #endif
+    // the lo / mid split: a group whose wave 0 runs BIP143 per-tx hashes
+    // before its chain (a witness input, or a fork-id network) gives the mid
+    // segment one window of the lo segment (HKV_BLK_K1_HASHED)
+    int k1 = BLK_K1;
+#if HKV_BLK_K1_HASHED
+    if constexpr (STD) {
+      const uint32_t* row_;
+      if (__any(blk_needs_tx_hashes(sa, base + (ln & (BLK_SIGS - 1)), n, row_))) k1 = HKV_BLK_K1_HASHED;
+    }
+#endif
     const int half = (int)(ln >> 5);
     const uint32_t c = (ln & 31u) >> 1;
     const uint32_t i = base + c;
@@ -1635,14 +1651,14 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
       fe_sel(V, V, q.y, m1);
       fe_sel(V, V, q.x, m0);  // x | y | 1 | 1
 #pragma unroll 1
-      for (int d = 0; d < QW * BLK_K1; ++d) quad_double(V, m0, m1, m2);
+      for (int d = 0; d < QW * k1; ++d) quad_double(V, m0, m1, m2);
       if (qd < 3) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) qpub[qd][k][cq] = V.v[k];
       }
       blk_post(&bflag[BF_Q], seq);
 #pragma unroll 1
-      for (int d = QW * BLK_K1; d < QW * BLK_K2; ++d) quad_double(V, m0, m1, m2);
+      for (int d = QW * k1; d < QW * BLK_K2; ++d) quad_double(V, m0, m1, m2);
       // to the chains' pair layout: X2 | Y2 with Z2 on both lanes; (X2, Y2) is
       // an affine point of the isomorphic curve of scale Z2
       const int src_p = (int)(4 * c + (odd ? 1u : 0u)), src_z = (int)(4 * c + 2);
@@ -1676,8 +1692,8 @@ __global__ void __launch_bounds__(BLK_TPB, 1) hkv_block_kernel(uint32_t* __restr
     const uint32_t flags = im[(size_t)IM_FLAGS * n_pad + i];
     const bool valid = (i < n) && (flags & FLAG_VALID);
     const bool negh = (flags & (half ? FLAG_NEG2 : FLAG_NEG1)) != 0;
-    const int w_hi = wv == 0 ? BLK_K1 - 1 : (wv == 1 ? NWIN - 1 : BLK_K2 - 1);
-    const int w_lo = wv == 0 ? 0 : (wv == 1 ? BLK_K2 : BLK_K1);
+    const int w_hi = wv == 0 ? k1 - 1 : (wv == 1 ? NWIN - 1 : BLK_K2 - 1);
+    const int w_lo = wv == 0 ? 0 : (wv == 1 ? BLK_K2 : k1);
     fe zs;  // the segment's isomorphic scale (formed before the chain: off the join's path)
     fe_mul(zs, Zg, zb);
     bool inf;
