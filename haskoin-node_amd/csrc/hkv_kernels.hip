@@ -1354,7 +1354,7 @@ __global__ void __launch_bounds__(PAIR_TPB, 2) hkv_pair_split_kernel(uint32_t* _
 #define HKV_BLK_K2 27
 #endif
 #ifndef HKV_BLK_K1_HASHED  // the lo / mid split of a group with BIP143 per-tx hashes on wave 0 (0: BLK_K1)
-#define HKV_BLK_K1_HASHED 0
+#define HKV_BLK_K1_HASHED 16
 #endif
 constexpr int BLK_K1 = HKV_BLK_K1, BLK_K2 = HKV_BLK_K2;
 static_assert(HKV_BLK_K1_HASHED == 0 || (HKV_BLK_K1_HASHED >= 2 && HKV_BLK_K1_HASHED < HKV_BLK_K2), "three segments");
