@@ -23,7 +23,9 @@ HBM before the timed region):
       "strong" (the total is fixed).
 One step = the verify of the rank's shard (prologue + ecmult + verdict ->
 bitmap) plus, for N > 1, the RCCL all-gather of the verdict bitmap (the only
-collective; hkv/shard.py ShardedVerify). value = all ranks' verifies /
+collective; hkv/shard.py ShardedVerify; --force-collective keeps it at N = 1
+through a one-rank RCCL group, a test of the device collective on a 1-GPU
+lease: the line then reads collective "rccl"). value = all ranks' verifies /
 max-over-ranks time. After the timed steps every rank checks its slice of
 the gathered bitmap against its labels and the counts are summed
 (`mismatches`: every bit of the global bitmap against its record's label).
@@ -855,7 +857,13 @@ def mock_main(args, world: int, rank: int) -> None:
     sys.path.insert(0, os.path.join(ROOT, "haskoin-node_amd"))
     from hkv.records import bits_from_bools
     from hkv.shard import ShardedVerify
-    if world > 1:
+    use_dist = world > 1 or args.force_collective
+    if use_dist:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("gloo")
     if os.environ.get("HKV_MOCK_FAIL_RANK") == str(rank):
         sys.exit(3)  # test hook: this rank dies inside the group, the others block in the all-gather
@@ -866,24 +874,25 @@ def mock_main(args, world: int, rank: int) -> None:
         bits.zero_()
         bits[: len(w)] = torch.from_numpy(w.view(np.int32))
 
-    sv = ShardedVerify(torch, n_total, rank, world, verify, dist=dist, device="cpu")
+    sv = ShardedVerify(torch, n_total, rank, world, verify, dist=dist if use_dist else None, device="cpu",
+                       force_collective=use_dist)
     for _ in range(args.warmup):
         sv.step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sv.step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     full = sv.bitmap()
     lab = bits_from_bools(mock_pattern(np.arange(sv.lo, sv.hi)).astype(bool))
     chk = torch.tensor([sv.slice_mismatches(full, lab)], dtype=torch.int64)
     devs = [{"rank": rank, "device": "cpu", "pid": os.getpid()}]
-    if world > 1:
+    if use_dist:
         dist.all_reduce(chk, op=dist.ReduceOp.SUM)
         gathered = [None] * world
         dist.all_gather_object(gathered, devs[0])
@@ -892,9 +901,11 @@ def mock_main(args, world: int, rank: int) -> None:
         dt = t.item()
         print(json.dumps({"metric": "mock", "mock": True, "value": round(n_total * args.steps / dt, 1),
                           "n_gpus": world, "ranks_seen": world, "rank_devices": devs, "steps": args.steps,
-                          "warmup": args.warmup, "mismatches": int(chk.item()), "global_batch": n_total}),
+                          "warmup": args.warmup, "mismatches": int(chk.item()), "global_batch": n_total,
+                          "collective": "gloo" if use_dist else None,
+                          "gather_vs_local_mismatches": sv.slice_mismatches(full, sv.local_bitmap())}),
               flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
@@ -926,6 +937,10 @@ def main() -> None:
                     help="test only: every rank runs on device 0 (the N > 1 code path on a 1-GPU lease); the "
                          "verdict words are all-gathered over gloo through host memory, since RCCL takes one rank "
                          "per GPU. Not a scaling measurement")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="test only: at WORLD_SIZE 1 still create the nccl (RCCL) group with device_id and run the "
+                         "step's all-gather of the verdict words on the device, on the stream libhkv enqueued on "
+                         "(the N > 1 collective path on a 1-GPU lease)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "latest_pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -954,12 +969,22 @@ def main() -> None:
         print(f"bench.py: rank {rank} needs GPU {gpu} but only {have} visible", file=sys.stderr, flush=True)
         sys.exit(2)
     torch.cuda.set_device(gpu)
-    if world > 1:
+    # the group: N > 1 ranks, or --force-collective at N = 1 (a one-rank RCCL
+    # group, so the device-side all-gather of the N > 1 step runs on one GPU)
+    use_dist = world > 1 or (args.force_collective and not share)
+    collective = None
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if share:
             dist.init_process_group("gloo")
+            collective = "gloo"
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            collective = "rccl" if torch.version.hip else "nccl"
     # the tensors the ranks reduce over: on the device for RCCL, in host
     # memory for gloo
     red_dev = "cpu" if share else "cuda"
@@ -987,7 +1012,8 @@ def main() -> None:
     def verify_shard(lo, hi, bits):
         v.verify_device(0, recs.data_ptr(), hi - lo, args.mode, bits.data_ptr(), sptr)
 
-    sv = ShardedVerify(torch, n_total, rank, world, verify_shard, dist=dist, gather_on_host=share)
+    sv = ShardedVerify(torch, n_total, rank, world, verify_shard, dist=dist if use_dist else None,
+                       gather_on_host=share, force_collective=use_dist)
     n = sv.local_n
     recs = torch.empty(n * 168, dtype=torch.uint8, device="cuda")
     labels = torch.zeros((n + 63) // 64 * 2, dtype=torch.int32, device="cuda")
@@ -1001,14 +1027,14 @@ def main() -> None:
         sv.step()
     torch.cuda.synchronize()
     v.lib.hkv_profile_enable(v.ctx, 1)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sv.step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     pm, em, nl = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
@@ -1019,7 +1045,7 @@ def main() -> None:
 
     t = torch.tensor([dt, em.value / max(1, nl.value), pm.value / max(1, nl.value)], dtype=torch.float64,
                      device=red_dev)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max, ecm_ms, pro_ms = t.tolist()
 
@@ -1029,13 +1055,20 @@ def main() -> None:
     # gathered bitmap is checked against the label of the same global record
     full = sv.bitmap()
     lab_np = labels.cpu().numpy().view(np.uint32)
+    # and the gathered bitmap's slice against the rank's own words as the
+    # verify wrote them (before the collective): a gather that lost, moved
+    # or raced a word shows here even where the labels would not
+    own = sv.local_bitmap()
     chk = torch.tensor([sv.slice_mismatches(full, lab_np),
                         int(np.unpackbits(full.view(np.uint8), bitorder="little")[sv.lo:sv.hi].sum()),
-                        int(np.unpackbits(lab_np.view(np.uint8), bitorder="little")[:n].sum())],
+                        int(np.unpackbits(lab_np.view(np.uint8), bitorder="little")[:n].sum()),
+                        sv.slice_mismatches(full, own)],
                        dtype=torch.int64, device=red_dev)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(chk, op=dist.ReduceOp.SUM)
-    mismatches, accepted, label_valid = chk.tolist()
+    mismatches, accepted, label_valid, gather_vs_local = chk.tolist()
+    import hashlib
+    bitmap_sha = hashlib.sha256(full[: (n_total + 31) // 32].tobytes()).hexdigest()[:32]
     # which device every rank ran on (the line proves N ranks on N GPUs)
     props = torch.cuda.get_device_properties(gpu)
     me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(), "name": props.name,
@@ -1043,7 +1076,7 @@ def main() -> None:
           "uuid": str(getattr(props, "uuid", "")) or None, "pid": os.getpid(), "local_n": n}
     rank_devices = [me]
     ranks_seen = 1
-    if world > 1:
+    if use_dist:
         ranks_seen = dist.get_world_size()
         rank_devices = [None] * world
         dist.all_gather_object(rank_devices, me)
@@ -1100,7 +1133,8 @@ def main() -> None:
                         f"seed 0x{seed:X}), contiguous 64-aligned shards, each rank generating only its slice; "
                         + ("one gloo all-gather of the verdict words through host memory per step (--share-device: "
                            "every rank on device 0; a test of the N > 1 code path, not a scaling point)" if share else
-                           "one RCCL all-gather of the verdict bitmap per step"))
+                           "one RCCL all-gather of the verdict bitmap per step" if collective == "rccl" else
+                           "no collective (one rank; --force-collective runs the RCCL all-gather at N = 1)"))
         else:
             workload = ("BASELINE configs[1]: 1,048,576 valid (hash,r,s,pubkey) per GPU, 90% compressed / 10% "
                         "uncompressed keys, 65,536-key pool")
@@ -1112,6 +1146,10 @@ def main() -> None:
             "ranks_seen": ranks_seen,
             "rank_devices": rank_devices,
             "share_device": share,
+            "collective": collective,
+            "force_collective": bool(args.force_collective and world == 1 and not share),
+            "gather_vs_local_mismatches": gather_vs_local,
+            "bitmap_sha256_128": bitmap_sha,
             "launcher": ("bench.py spawn" if os.environ.get("HKV_BENCH_SPAWNED") else
                          "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or "GROUP_RANK" in os.environ else
                          "external" if world > 1 else "single process"),
@@ -1163,7 +1201,7 @@ def main() -> None:
         }
         print(json.dumps(line), flush=True)
     v.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

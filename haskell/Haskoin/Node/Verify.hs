@@ -42,20 +42,23 @@ module Haskoin.Node.Verify
   )
 where
 
-import Control.Monad (forM_, forever, when)
+import Control.Monad (forM_, when)
 import Control.Monad.Logger (MonadLoggerIO, logDebugS, logWarnS)
+import Data.Array (listArray, (!))
 import Crypto.Secp256k1 (getCompactSig)
 import Data.Bits (shiftR, testBit, (.&.))
 import Data.ByteString (ByteString)
 import qualified Data.ByteString as B
 import qualified Data.ByteString.Unsafe as BU
+import qualified Data.Text as T
 import Data.Word (Word32, Word64, Word8)
 import Foreign.C.String (peekCString)
+import GHC.Clock (getMonotonicTimeNSec)
 import Foreign.Marshal.Alloc (alloca)
-import Foreign.Marshal.Array (allocaArray, peekArray, withArray)
+import Foreign.Marshal.Array (allocaArray, withArray)
 import Foreign.Marshal.Utils (copyBytes, fillBytes, with)
 import Foreign.Ptr (Ptr, castPtr, plusPtr)
-import Foreign.Storable (peek, pokeByteOff)
+import Foreign.Storable (peek, peekElemOff, pokeByteOff)
 import Haskoin
   ( Block (..),
     BlockHash,
@@ -75,6 +78,7 @@ import Haskoin
     runPutS,
     serialize,
     txHash,
+    verifyStdInput,
   )
 import Haskoin.Node.Verify.FFI
 import NQE (Mailbox, Publisher, newMailbox, publish, receive, send)
@@ -88,6 +92,8 @@ import UnliftIO
     liftIO,
     newMVar,
     throwIO,
+    timeout,
+    try,
     withAsync,
     withMVar,
   )
@@ -155,9 +161,12 @@ pokeRecord p (msg, sig, pub) = do
       BU.unsafeUseAsCStringLen bs $ \(src, len) ->
         copyBytes (dst `plusPtr` off) (castPtr src) (min n len)
 
--- | Bit i of word i/32 is verdict i.
-readBits :: Int -> [Word32] -> [Bool]
-readBits n ws = [testBit (ws !! (i `shiftR` 5)) (i .&. 31) | i <- [0 .. n - 1]]
+-- | Bit i of word i/32 is verdict i. O(n): one peekElemOff per verdict
+-- straight from the verdict buffer (no list indexing).
+readBits :: Int -> Ptr Word32 -> IO [Bool]
+readBits n p = mapM bit [0 .. n - 1]
+  where
+    bit i = (`testBit` (i .&. 31)) <$> peekElemOff p (i `shiftR` 5)
 
 -- | Raw (msg32, compact r||s, SEC1 pubkey bytes) tuples; mode 'hkvLibsecp'
 -- is secp256k1_ecdsa_verify, 'hkvHaskoin' is verifyHashSig. Batches larger
@@ -172,7 +181,7 @@ verifyRawBatch v mode = fmap concat . mapM one . chunks v.capacity
       forM_ (zip [0 ..] xs) $ \(i, t) -> pokeRecord (recs `plusPtr` (i * hkvRecordSize)) t
       allocaArray nw $ \bits -> do
         c_hkv_verify v.ctx v.batch (fromIntegral n) mode bits >>= check "hkv_verify" . fromIntegral
-        readBits n <$> peekArray nw bits
+        readBits n bits
 
 chunks :: Int -> [a] -> [[a]]
 chunks _ [] = []
@@ -210,19 +219,31 @@ verifyStdInputBatch v net txs ins = withMVar v.lock $ \_ -> do
             allocaArray nw $ \bits -> do
               c_hkv_verify_std_inputs v.ctx ptxs pjobs (fromIntegral n) forkid bits
                 >>= check "hkv_verify_std_inputs" . fromIntegral
-              readBits n <$> peekArray nw bits
+              readBits n bits
 
 -- ---------------------------------------------------------------------------
 -- The Verify actor (withChain idiom, Chain.hs:277-307)
+--
+-- Mirrored, policy for policy, by haskoin-node_amd/hkv/actor.py (VerifyActor),
+-- which tests/test_gpu_actor.py runs on the GPU.
 
 -- | Where the prevouts come from: the node keeps no UTXO set (headers only,
 -- Chain.hs:209-231), so the application supplies (tx index, input index,
 -- prevout script, amount) for every input it wants checked.
 data VerifyConfig = VerifyConfig
   { net :: !Network,
+    -- | secp256k1-haskell context for the CPU re-verify of a failed batch
+    secp :: !Ctx,
     verifier :: !Verifier,
     prevouts :: !(Block -> IO [(Int, Int, ScriptOutput, Word64)]),
     txPrevouts :: !(Tx -> IO [(Int, ScriptOutput, Word64)]),
+    -- | mempool txs are coalesced into one GPU call of at most this many
+    -- inputs (16,384: the pair kernel's range, DESIGN.md §4.2)...
+    maxInputs :: !Int,
+    -- | ...or of what arrived within this many microseconds of the first
+    maxWaitMicros :: !Int,
+    -- | GPU re-submissions of a batch whose call failed before the CPU path
+    retries :: !Int,
     -- | verdicts are published here
     pub :: !(Publisher VerifyEvent)
   }
@@ -239,29 +260,93 @@ data VerifyMessage
 
 newtype VerifyActor = VerifyActor (Mailbox VerifyMessage)
 
--- | Start the actor; it lives as long as the continuation.
+-- | Start the actor; it lives as long as the continuation. A failed GPU
+-- call never reaches 'link': 'verifyWithPolicy' catches 'VerifierException'.
 withVerifyActor :: (MonadUnliftIO m, MonadLoggerIO m) => VerifyConfig -> (VerifyActor -> m a) -> m a
 withVerifyActor cfg action = do
   (inbox, mailbox) <- newMailbox
   $(logDebugS) "Verify" "Starting verify actor"
-  withAsync (run inbox) $ \a -> link a >> action (VerifyActor mailbox)
+  withAsync (run inbox Nothing) $ \a -> link a >> action (VerifyActor mailbox)
   where
-    run inbox = forever $ receive inbox >>= handle
-    handle (VerifyBlock b) = do
+    -- held: what was taken from the mailbox while a tx batch was formed and
+    -- did not fit it (a block, or a tx past maxInputs); it is handled next
+    run inbox held = do
+      p <- maybe (PendingMsg <$> receive inbox) return held
+      case p of
+        PendingMsg (VerifyBlock b) -> handleBlock b >> run inbox Nothing
+        PendingMsg (VerifyTx t) -> liftIO (cfg.txPrevouts t) >>= batchFrom inbox t
+        PendingTx t ins -> batchFrom inbox t ins
+    batchFrom inbox t ins = do
+      t0 <- liftIO getMonotonicTimeNSec
+      (batch, held') <- collect inbox t0 [(t, ins)] (length ins)
+      handleTxs batch
+      run inbox held'
+    -- coalesce VerifyTx messages: drain the mailbox until the batch holds
+    -- maxInputs inputs or maxWaitMicros have passed since its first tx
+    collect inbox t0 acc n
+      | n >= cfg.maxInputs = return (reverse acc, Nothing)
+      | otherwise = do
+          now <- liftIO getMonotonicTimeNSec
+          let left = cfg.maxWaitMicros - fromIntegral ((now - t0) `div` 1000)
+          mm <- if left <= 0 then return Nothing else timeout left (receive inbox)
+          case mm of
+            Nothing -> return (reverse acc, Nothing)
+            Just (VerifyTx t) -> do
+              ins <- liftIO (cfg.txPrevouts t)
+              if n + length ins > cfg.maxInputs
+                then return (reverse acc, Just (PendingTx t ins))
+                else collect inbox t0 ((t, ins) : acc) (n + length ins)
+            Just other -> return (reverse acc, Just (PendingMsg other))
+    handleBlock b = do
       ins <- liftIO (cfg.prevouts b)
-      ok <- liftIO (verifyStdInputBatch cfg.verifier cfg.net b.txs ins)
+      let h = headerHash b.header
+      ok <- verifyWithPolicy cfg b.txs ins
       let bad = [(t, i) | ((t, i, _, _), False) <- zip ins ok]
-          h = headerHash b.header
       if null bad
         then publish (BlockVerified h) cfg.pub
         else do
           $(logWarnS) "Verify" "Block has inputs that fail verifyStdInput"
           publish (BlockRejected h bad) cfg.pub
-    handle (VerifyTx t) = do
-      ins <- liftIO (cfg.txPrevouts t)
-      ok <- liftIO (verifyStdInputBatch cfg.verifier cfg.net [t] [(0, i, so, val) | (i, so, val) <- ins])
-      let bad = [i | ((i, _, _), False) <- zip ins ok]
-      publish (if null bad then TxVerified (txHash t) else TxRejected (txHash t) bad) cfg.pub
+    -- one GPU call for the whole coalesced batch: tx k of the batch is tx
+    -- index k of the call
+    handleTxs batch = do
+      let txs = map fst batch
+          ins = [(k, i, so, val) | (k, (_, xs)) <- zip [0 ..] batch, (i, so, val) <- xs]
+      ok <- if null ins then return [] else verifyWithPolicy cfg txs ins
+      -- the verdicts in batch order, cut per tx (one pass)
+      forM_ (zip batch (splitPlaces (map (length . snd) batch) ok)) $ \((t, xs), vs) -> do
+        let bad = [i | ((i, _, _), False) <- zip xs vs]
+        publish (if null bad then TxVerified (txHash t) else TxRejected (txHash t) bad) cfg.pub
+    splitPlaces [] _ = []
+    splitPlaces (c : cs) xs = let (a, b) = splitAt c xs in a : splitPlaces cs b
+
+-- | What the actor handles next: a message from the mailbox, or a tx whose
+-- prevouts were looked up while a batch was formed that it did not fit.
+data Pending
+  = PendingMsg !VerifyMessage
+  | PendingTx !Tx ![(Int, ScriptOutput, Word64)]
+
+-- | The error policy (SURVEY.md §5 failure detection): a failed GPU call
+-- (any 'VerifierException': HKV_E_INTERNAL when the call's multisig tail
+-- gave up, a device error) is re-submitted up to 'retries' times; then the
+-- batch is re-verified on the CPU with haskoin-core's own per-input
+-- 'verifyStdInput' (the path the drop-in replaces). Nothing is thrown, so
+-- 'link' never takes the node down for a verify failure.
+verifyWithPolicy ::
+  (MonadUnliftIO m, MonadLoggerIO m) => VerifyConfig -> [Tx] -> [(Int, Int, ScriptOutput, Word64)] -> m [Bool]
+verifyWithPolicy cfg txs ins = attempt (cfg.retries + 1)
+  where
+    attempt k = do
+      r <- liftIO (try (verifyStdInputBatch cfg.verifier cfg.net txs ins))
+      case r of
+        Right ok -> return ok
+        Left (VerifierException msg rc) -> do
+          $(logWarnS) "Verify" ("GPU batch failed (" <> T.pack msg <> ", rc " <> T.pack (show rc) <> ")")
+          if k > 1 then attempt (k - 1) else cpu
+    arr = listArray (0, length txs - 1) txs
+    cpu = do
+      $(logWarnS) "Verify" "Re-verifying the batch on the CPU (verifyStdInput)"
+      return [verifyStdInput cfg.net cfg.secp (arr ! t) i so val | (t, i, so, val) <- ins]
 
 -- | Forward a block from PeerEvent (PeerMessage _ (MBlock b)) (Node.hs:172).
 verifyBlock :: (MonadIO m) => Block -> VerifyActor -> m ()

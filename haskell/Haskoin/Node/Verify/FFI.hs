@@ -23,6 +23,9 @@ module Haskoin.Node.Verify.FFI
     c_hkv_batch_capacity,
     c_hkv_verify,
     c_hkv_verify_std_inputs,
+    c_hkv_verify_std_inputs_device_status,
+    c_hkv_device_fault,
+    c_hkv_device_healthy,
     c_hkv_check_headers,
     c_hkv_merkle_roots,
     c_hkv_strerror,
@@ -30,6 +33,8 @@ module Haskoin.Node.Verify.FFI
     hkvHaskoin,
     hkvRecordSize,
     hkvNoForkId,
+    hkvEInternal,
+    hkvStatusTailFault,
   )
 where
 
@@ -110,6 +115,16 @@ hkvRecordSize = 168 -- msg32 | r | s | pklen | pubkey[65] | pad[6]
 hkvNoForkId :: Int32
 hkvNoForkId = -1
 
+-- | HKV_E_INTERNAL: what hkv_verify_std_inputs returns when its own call's
+-- multisig tail reported HKV_STATUS_TAIL_FAULT (some multisig verdicts were
+-- left at 0); the actor re-submits the batch (Verify.hs verifyWithPolicy).
+hkvEInternal :: CInt
+hkvEInternal = -5
+
+-- | HKV_STATUS_TAIL_FAULT, the bit the _status form and hkv_device_fault report.
+hkvStatusTailFault :: Word32
+hkvStatusTailFault = 1
+
 -- Context / batch lifetime: cheap, may use `unsafe`.
 foreign import ccall safe "hkv_open"
   c_hkv_open :: CInt -> Word32 -> Ptr (Ptr HkvCtx) -> IO CInt
@@ -136,6 +151,20 @@ foreign import ccall safe "hkv_verify"
 
 foreign import ccall safe "hkv_verify_std_inputs"
   c_hkv_verify_std_inputs :: Ptr HkvCtx -> Ptr HkvTxs -> Ptr InputJob -> CSize -> Int32 -> Ptr Word32 -> IO CInt
+
+-- The asynchronous block path: everything is enqueued on the caller's HIP
+-- stream (the last argument); d_status gets HKV_STATUS_* bits ORed in on it.
+foreign import ccall safe "hkv_verify_std_inputs_device_status"
+  c_hkv_verify_std_inputs_device_status ::
+    Ptr HkvCtx -> CInt -> Ptr HkvTxs -> Ptr InputJob -> CSize -> Int32 -> Ptr () -> Ptr Word32 -> Ptr Word32 ->
+    Ptr () -> IO CInt
+
+-- Read and clear device dev's sticky fault latch (waits for its enqueued calls).
+foreign import ccall safe "hkv_device_fault"
+  c_hkv_device_fault :: Ptr HkvCtx -> CInt -> Ptr Word32 -> IO CInt
+
+foreign import ccall unsafe "hkv_device_healthy"
+  c_hkv_device_healthy :: Ptr HkvCtx -> CInt -> IO CInt
 
 foreign import ccall safe "hkv_check_headers"
   c_hkv_check_headers ::

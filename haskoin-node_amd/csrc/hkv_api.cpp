@@ -96,8 +96,6 @@ struct DevCtx {
   // previous user's work (this event) before enqueueing and records it after,
   // so calls on different streams run in enqueue order instead of racing.
   hipEvent_t last_use = nullptr;
-  hipStream_t last_stream = nullptr;  // the stream last_use was recorded on (valid: last_valid)
-  bool last_valid = false;
   uint32_t inject = 0;  // hkv_debug_fail_device: HKV_FAIL_* of this device's next host-batch shard
 };
 
@@ -159,8 +157,8 @@ constexpr size_t MS_BAR_WORDS = 32, MS_FAULT = 16, MS_HOST_STATUS = 17;  // DevC
 #ifndef HKV_HOST_FIRST_DIV  // the host-batch path's first chunk: one resident grid / this
 #define HKV_HOST_FIRST_DIV 4
 #endif
-#ifndef HKV_TAIL_BLOCK_GRID
-#define HKV_TAIL_BLOCK_GRID 4096
+#ifndef HKV_HOST_MAX_GRIDS  // the host-batch path's largest chunk, in resident grids
+#define HKV_HOST_MAX_GRIDS 8
 #endif
 
 int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
@@ -184,18 +182,17 @@ int ensure_dev_buffers(DevCtx& d, size_t n_pad) {
 
 // Order a call on stream st after the previous user of the device's scratch
 // (acquire) and publish st as the new last user (release). Callers hold ctx->mu.
+// The wait is taken on every call, whatever stream the last release used: a
+// stream handle equal to the last one does not prove the same stream
+// (hipStreamPerThread maps to a different stream per thread, and a destroyed
+// stream's handle can be reused), and skipping it measured within noise
+// (profiles/r05c/ab_skip_wait.txt).
 int scratch_acquire(DevCtx& d, hipStream_t st) {
-  // (a call on the stream of the last release is ordered after it already:
-  // one HIP call less in front of a block's first launch)
-  if (d.last_valid && st == d.last_stream) return HKV_OK;
   HKV_TRY(hipStreamWaitEvent(st, d.last_use, 0), "hipStreamWaitEvent(scratch)");
   return HKV_OK;
 }
 int scratch_release(DevCtx& d, hipStream_t st) {
-  d.last_valid = false;
   HKV_TRY(hipEventRecord(d.last_use, st), "hipEventRecord(scratch)");
-  d.last_stream = st;
-  d.last_valid = true;
   return HKV_OK;
 }
 
@@ -640,9 +637,10 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
     if (rc) return rc;
   }
   // (operands taken after every launch before it has sized the scratch)
-  // (a block-sized batch: a smaller tail grid, which a block without
-  // multisig inputs launches and retires sooner)
-  const uint32_t tail_grid = fused_scan ? std::min<uint32_t>((uint32_t)d.n_cu, HKV_TAIL_BLOCK_GRID) : (uint32_t)d.n_cu;
+  // (one workgroup per CU on every path: the tail's scratch slots are sized
+  // by n_cu, hkv_internal.h launch_ms_tail; a smaller grid for block-sized
+  // batches measured no different, profiles/r05k/tail_grid_ab.txt)
+  const uint32_t tail_grid = (uint32_t)d.n_cu;
   HKV_TRY(hkv::launch_ms_tail(tail_args(d, dt, jobs, n, forkid, out_bits, fused, ms, cap_cand), tail_grid, st),
           "multisig tail launch");
   ++d.tail_epoch;  // (launched: it zeroes the slot and the scan sum the next call uses)
@@ -879,13 +877,26 @@ static int enqueue_host_shard(DevCtx& d, const uint8_t* host, const hkv::Shard& 
   // with a one-grid first chunk and 10.75 / 10.69 with an eighth; one
   // quarter of the shard per chunk, the earlier schedule, exposed a
   // quarter-shard H2D before the first verify: 16M 161 ms, now 146 ms.)
+  // Growth stops at HKV_HOST_MAX_GRIDS grids (a chunk of 8 grids verifies
+  // for ~18 ms, far above a launch's cost), and the intermediate buffers are
+  // sized once for the schedule's largest chunk before the first copy: a
+  // buffer grown inside the loop would hipFree (a device-wide sync) between
+  // chunks and lose the overlap.
   const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
   const uint8_t* src = host + s.lo * hkv::REC_SIZE;
-  size_t next = len >= 2 * grid_lanes ? grid_lanes / HKV_HOST_FIRST_DIV : len;
-  for (size_t off = 0, cl = 0; off < len && !rc; off += cl) {
-    cl = std::min(next, len - off);
+  const size_t first = len >= 2 * grid_lanes ? grid_lanes / HKV_HOST_FIRST_DIV : len;
+  auto step = [&](size_t off, size_t& next) {
+    size_t cl = std::min(next, len - off);
     if (len - off - cl < grid_lanes) cl = len - off;
-    next = std::min(std::max(2 * next, grid_lanes), (size_t)1 << 40);
+    next = std::min(std::max(2 * next, grid_lanes), (size_t)HKV_HOST_MAX_GRIDS * grid_lanes);
+    return cl;
+  };
+  size_t largest = 0;
+  for (size_t off = 0, next = first, cl = 0; off < len; off += cl) largest = std::max(largest, cl = step(off, next));
+  rc = ensure_dev_buffers(d, round_up(largest, hkv::WG));
+  size_t next = first;
+  for (size_t off = 0, cl = 0; off < len && !rc; off += cl) {
+    cl = step(off, next);
     hipEvent_t ev = nullptr;
     hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) {

@@ -51,18 +51,22 @@ class ShardedVerify:
     verify: called as verify(lo, hi, bits) — must write the verdict words of
     records [lo, hi) into the int32 tensor ``bits`` (hkv_verify_device on the
     rank's GPU in bench.py; a CPU checker in the gloo tests).
-    dist: torch.distributed (None or world == 1: no collective).
+    dist: torch.distributed (None, or world == 1 without force_collective:
+    no collective).
+    force_collective: keep the all-gather at world == 1 (bench.py
+    --force-collective: a one-rank RCCL group, so the N > 1 step's device
+    collective runs on a 1-GPU lease).
     gather_on_host: the all-gather runs on host copies of the words (a gloo
     group: bench.py --share-device, every rank on one GPU, which RCCL does
     not allow)."""
 
     def __init__(self, torch, n: int, rank: int, world: int, verify: Callable, dist=None, device: str = "cuda",
-                 gather_on_host: bool = False):
+                 gather_on_host: bool = False, force_collective: bool = False):
         self.n, self.rank, self.world = n, rank, world
         self.lo, self.hi = shard_bounds(n, rank, world)
         self.wpr = words_per_rank(n, world)
         self.verify = verify
-        self.dist = dist if world > 1 else None
+        self.dist = dist if (world > 1 or force_collective) else None
         self.bits = torch.zeros(self.wpr, dtype=torch.int32, device=device)
         gdev = "cpu" if gather_on_host else device
         self.host_bits = torch.zeros(self.wpr, dtype=torch.int32, device="cpu") \
@@ -82,6 +86,11 @@ class ShardedVerify:
                 self.dist.all_gather_into_tensor(self.gathered, self.host_bits)
             else:
                 self.dist.all_gather_into_tensor(self.gathered, self.bits)
+
+    def local_bitmap(self) -> np.ndarray:
+        """This rank's own verdict words for records [lo, hi) as verify()
+        wrote them (before any collective): ceil((hi - lo) / 32) words."""
+        return self.bits.cpu().numpy().view(np.uint32)[: (self.hi - self.lo + 31) // 32].copy()
 
     def bitmap(self) -> np.ndarray:
         """The global verdict bitmap (ceil(n/32) words) after step()."""

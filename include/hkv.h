@@ -115,9 +115,11 @@ int hkv_device_failures(hkv_ctx* ctx, int dev);
 #define HKV_FAIL_ENQUEUE 1u
 #define HKV_FAIL_JOIN 2u
 #define HKV_FAIL_ALLOC 3u
-/* HKV_FAIL_TAIL: the next multisig tail launch on device k takes its grid
- * barrier's timeout branch at once (as if its workgroups were not
- * co-resident), so the fault reporting below can be tested. */
+/* HKV_FAIL_TAIL: the next multisig tail launch on device k gives up the
+ * first wait of its work queue at a phase transition (the timeout branch of a
+ * wait for the phase before, taken at once without looking at the count), so
+ * the fault reporting below can be tested; deterministic for any batch with a
+ * multisig input. */
 #define HKV_FAIL_TAIL 4u
 int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when);
 
@@ -248,9 +250,8 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * replayed on device (count == m and all keys valid).
  * ASYNCHRONOUS: everything is enqueued on hip_stream and the call returns
  * without waiting for any of it (the batch's multisig record count stays on
- * the device: the tail — inside the block kernel for a block-sized batch,
- * else one launch after the verify — reads it and does nothing when it is
- * 0), so a
+ * the device: the tail, one launch after the verify on every path, reads it
+ * and does nothing when it is 0), so a
  * caller may enqueue block k+1 while block k verifies, and hip_stream may be
  * gated on events recorded after the call. Batches run in chunks of 131,072
  * inputs (the multisig scratch is sized per chunk by its 16-of-16 bound, 136

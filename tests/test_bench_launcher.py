@@ -75,3 +75,21 @@ def test_failing_rank_stops_the_launch():
     assert r.returncode == 3
     assert "stopping the others" in r.stderr
     assert time.time() - t0 < 90
+
+
+def test_force_collective_keeps_the_gather_at_one_rank():
+    """--force-collective at WORLD_SIZE 1 (no launcher): the one-rank group is
+    created and the step's all-gather runs (gloo in the mock leg; the GPU leg
+    creates the nccl group, tests/test_gpu_collective.py), and the gathered
+    bitmap equals the rank's own words and the pattern."""
+    n = 4096 + 97
+    r = subprocess.run([sys.executable, BENCH, "--mock-cpu", "--force-collective", "--steps", "2", "--warmup", "1",
+                        "--config4-n", str(n)], capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["collective"] == "gloo" and d["n_gpus"] == 1
+    assert d["mismatches"] == 0 and d["gather_vs_local_mismatches"] == 0
+    r = subprocess.run([sys.executable, BENCH, "--mock-cpu", "--steps", "1", "--warmup", "0",
+                        "--config4-n", str(n)], capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])["collective"] is None
