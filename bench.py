@@ -162,6 +162,51 @@ def steady_rate(fn, recs, mode: int, threads: int, min_s: float, per_thread: int
             "verdicts": out[:n0].astype(bool)}
 
 
+def smt_pair() -> tuple:
+    """Two CPUs of this job's affinity mask that are SMT siblings of one
+    physical core (sysfs thread_siblings_list), or None."""
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return None
+    for c in reversed(aff):  # (from the top: CPU 0 takes most of the host's interrupts)
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                txt = f.read().strip()
+        except OSError:
+            continue
+        sib = set()
+        for part in txt.split(","):
+            a, _, b = part.partition("-")
+            sib.update(range(int(a), int(b or a) + 1))
+        others = sorted(x for x in sib if x != c and x in aff)
+        if others:
+            return c, others[0]
+    return None
+
+
+def smt_core_rate(fn, recs, mode: int, min_s: float) -> dict:
+    """One physical core, measured: fn at 1 thread pinned to one CPU, then at
+    2 threads pinned to that CPU and its SMT sibling (threads inherit the
+    caller's affinity), each >= min_s in steady state. core_rate_smt is what
+    one physical core delivers with both hardware threads busy."""
+    pair = smt_pair()
+    if pair is None:
+        return {"skipped": "no SMT sibling pair in this job's affinity mask"}
+    old = os.sched_getaffinity(0)
+    try:
+        os.sched_setaffinity(0, {pair[0]})
+        one = steady_rate(fn, recs, mode, 1, min_s)
+        os.sched_setaffinity(0, set(pair))
+        two = steady_rate(fn, recs, mode, 2, min_s)
+    finally:
+        os.sched_setaffinity(0, old)
+    one.pop("verdicts")
+    two.pop("verdicts")
+    return {"cpus": list(pair), "one_thread": one, "two_threads_smt": two, "core_rate_1t": one["rate"],
+            "core_rate_smt": two["rate"], "smt_gain": round(two["rate"] / one["rate"], 3)}
+
+
 def cpu_baseline(samples, sweep, min_s: float = 1.0) -> dict:
     """The CPU leg (oracle/ is timed here and used as the checker here only).
 
@@ -251,13 +296,17 @@ def cpu_baseline(samples, sweep, min_s: float = 1.0) -> dict:
     quota_point["effective_cpus"] = round(quota_point["cpu_s"] / quota_point["wall_s"], 2)
     rate, cores = quota_point["rate"], q_threads
     phys = physical_cores(host)
+    smt = smt_core_rate(impls["secpfast"], np.ascontiguousarray(samples[0][1]), samples[0][2], max(2.0, 2 * min_s))
+    smt_rate = smt.get("core_rate_smt")
     first = samples[0][0]
     return {"value": rate, "unit": "verifies/s", "cores": cores, "kind": "port", "impl": "secpfast",
             "value_point": quota_point,
             "best_of_sweep": {"rate": best[0], "threads": best[1]},
             "kind_note": "a port of the reference library's algorithm: oracle/secp_fast.c restates libsecp256k1's "
                          "verify (5x52 field, GLV + wNAF5, w=15 G tables, safegcd, the pubkey parse / sqrt); "
-                         "libsecp256k1 itself is not installed on the box and not in /root/reference",
+                         "libsecp256k1 itself is not installed on the box and not in /root/reference. Its speed "
+                         "relative to libsecp256k1 (x86-64 asm field, tuned tables) is unmeasured, so every GPU/CPU "
+                         "ratio against it is an UPPER bound on the ratio against the real library",
             "sample": f"BASELINE configs[0]: the 4,000 inputs of the 2,000-tx P2PKH block (records extracted on "
                       f"device, HKV_HASKOIN = verifyHashSig), tiled to 2,000 records per thread per call; value = "
                       f"the steady rate at {cores} threads (this job's cgroup CPU quota, {quota} CPUs) over >= "
@@ -273,9 +322,14 @@ def cpu_baseline(samples, sweep, min_s: float = 1.0) -> dict:
                             "ok": bool(max(best[0], rate) <= quota * single * 1.1) if quota and single else None,
                             "note": "no point may exceed quota x single-thread rate x 1.1 (steady state)"},
             "whole_host": {"physical_cores": phys,
+                           "smt_extrapolated_value": round(smt_rate * phys, 1) if smt_rate and phys else None,
                            "extrapolated_value": round(per_core * phys, 1) if per_core and phys else None,
-                           "note": "per_core_value x the host's physical cores (lscpu): an extrapolation, not a "
-                                   "measurement (the job may use only its cgroup quota)"},
+                           "smt_core": smt,
+                           "note": "smt_extrapolated_value = one physical core's measured rate with both SMT "
+                                   "threads busy (smt_core: 2 threads pinned to sibling CPUs) x the host's physical "
+                                   "cores (lscpu); extrapolated_value = the 1-thread per-CPU-second rate x the "
+                                   "physical cores (ignores SMT). Both are extrapolations, not measurements (the "
+                                   "job may use only its cgroup quota); the SMT one is the higher CPU rate"},
             "thread_sweep": list(sweep), "samples": res, "host": host}
 
 
@@ -284,15 +338,19 @@ def north_star_ratio(value: float, cpu: dict) -> dict:
     MI355X". The whole-host figure is the extrapolation (per-core rate x
     physical cores); the quota-bound figure is what this job measured."""
     wh = (cpu.get("whole_host") or {}).get("extrapolated_value")
-    out = {"whole_host_extrapolated": round(value / wh, 1) if wh else None,
+    whs = (cpu.get("whole_host") or {}).get("smt_extrapolated_value")
+    out = {"whole_host_smt_extrapolated": round(value / whs, 1) if whs else None,
+           "whole_host_extrapolated": round(value / wh, 1) if wh else None,
            "quota_bound": round(value / cpu["value"], 1) if cpu.get("value") else None,
            "single_thread": round(value / cpu["single_thread_value"], 1) if cpu.get("single_thread_value") else None,
            "target": 50.0}
-    out["target_met_whole_host"] = bool(out["whole_host_extrapolated"] >= 50.0) \
-        if out["whole_host_extrapolated"] is not None else None
-    out["note"] = ("value (configs[1], HBM-resident) / the CPU rates: whole_host_extrapolated is the north_star "
-                   "reading (all host cores, extrapolated from the per-core rate); quota_bound is against this "
-                   "job's cgroup CPU share (measured)")
+    low = out["whole_host_smt_extrapolated"] or out["whole_host_extrapolated"]
+    out["target_met_whole_host"] = bool(low >= 50.0) if low is not None else None
+    out["note"] = ("value (configs[1], HBM-resident) / the CPU rates. The north_star reading is against all host "
+                   "cores, extrapolated: whole_host_smt_extrapolated (each physical core with both SMT threads, "
+                   "measured on one core) is the lower, stricter ratio and decides target_met_whole_host; "
+                   "whole_host_extrapolated ignores SMT. Both are upper bounds against libsecp256k1 itself "
+                   "(cpu_baseline.kind_note); quota_bound is against this job's cgroup CPU share (measured)")
     return out
 
 
@@ -494,24 +552,22 @@ def native_caller(txs, inputs, calls: int = 20) -> dict:
         shutil.rmtree(d, ignore_errors=True)
 
 
-def cpu_sighash_leg(txs, inputs, gpu_records) -> dict:
-    """Host side of configs[0]'s sighash (the CPU leg): the Python restatement
-    of verifyStdInput's non-ECDSA half (tx parse, txSigHash, decodeTxSig,
-    HASH160 template check; oracle/sighash_oracle.py) over the block's inputs,
-    timed single-threaded, and its records compared byte for byte with the
-    GPU's (msg32 = the sighash)."""
+def config0_records_check(txs, inputs, gpu_records) -> dict:
+    """configs[0]'s device-extracted records against the oracle
+    (oracle/sighash_oracle.py: tx parse, txSigHash, decodeTxSig, HASH160
+    template check) byte for byte — a parity check, not a CPU rate: the
+    Python restatement's speed says nothing about haskoin-core's sighash, so
+    it is not timed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import sighash_oracle as sh
-    t0 = time.perf_counter()
     parsed = [sh.tx_parse(t) for t in txs]
     exp = b"".join(sh.std_input_record(parsed[t], i, p, val) for (t, i, p, val) in inputs)
-    dt = time.perf_counter() - t0
     got = gpu_records.tobytes()
     n = len(inputs)
     rec_mism = sum(got[k * 168:(k + 1) * 168] != exp[k * 168:(k + 1) * 168] for k in range(n))
     msg_mism = sum(got[k * 168:k * 168 + 32] != exp[k * 168:k * 168 + 32] for k in range(n))
-    return {"inputs": n, "inputs_per_s_1_thread": round(n / dt, 1), "record_mismatches_vs_gpu": int(rec_mism),
-            "msg32_mismatches_vs_gpu": int(msg_mism), "impl": "oracle/sighash_oracle.py (Python, 1 thread)"}
+    return {"inputs": n, "record_mismatches_vs_oracle": int(rec_mism), "msg32_mismatches_vs_oracle": int(msg_mism),
+            "checker": "oracle/sighash_oracle.py"}
 
 
 def host_path(v, recs, n: int, steps: int) -> dict:
@@ -1095,6 +1151,7 @@ def main() -> None:
         single = world == 1 and not config4  # the N = 1 headline run carries the other legs
         if single and not args.no_config0:
             c0, c0_recs, c0_got, c0_txs, c0_inputs = config0_block(v, torch, args.steps)
+            c0["records_vs_oracle"] = config0_records_check(c0_txs, c0_inputs, c0_recs)
         if single and not args.no_block_mix:
             mix = block_mix(v, torch, args.steps)
         if single and not args.no_host_path:
@@ -1125,8 +1182,7 @@ def main() -> None:
             # north_star: ">= 50x the all-core host libsecp256k1 verify rate"
             if cpu.get("value"):
                 cpu["gpu_over_cpu"] = north_star_ratio(value, cpu)
-            if c0_recs is not None:
-                cpu["config0_host_sighash"] = cpu_sighash_leg(c0_txs, c0_inputs, c0_recs)
+
         if config4:
             workload = (f"BASELINE configs[4]: one IBD-style batch of {n_total:,} records (configs[1] distribution "
                         f"plus {inv / 10:g}% invalid: flipped msg32 / r / s bit, another key, the negated key; "

@@ -13,6 +13,7 @@ from .merkle import merkle_roots, merkle_roots_device
 from .sighash import TxBatch, tx_sig_hash_batch, verify_std_inputs
 from .verify import (Verifier, VerifierConfig, verify_hash_sig_batch,
                      verify_raw_batch)
+from .actor import VerifyActor, VerifyActorConfig
 
 __all__ = [
     "HKV_HASKOIN", "HKV_LIBSECP", "HKV_RECORD_SIZE", "HkvError", "lib_path",
@@ -20,5 +21,5 @@ __all__ = [
     "VerifierConfig", "verify_hash_sig_batch", "verify_raw_batch", "HKV_NO_FORKID",
     "HKV_SIGHASH_FORKID", "HKV_SIGHASH_LEGACY", "HkvTxs", "TxBatch", "tx_sig_hash_batch",
     "verify_std_inputs", "check_headers", "check_headers_device",
-    "merkle_roots", "merkle_roots_device",
+    "merkle_roots", "merkle_roots_device", "VerifyActor", "VerifyActorConfig",
 ]

@@ -134,3 +134,31 @@ def test_faster_than_port(fast, coracle):
         return best
 
     assert rate(fast.hkvo_fast_verify_batch) >= 2 * rate(coracle.hkvo_verify_batch)
+
+
+def test_cpu_baseline_reports_both_whole_host_extrapolations(coracle, monkeypatch):
+    """bench.py's CPU leg on a small sample (short points): the SMT-core
+    point (1 thread on one CPU, then 2 threads on it and a sibling; the
+    sibling pair is forced to two CPUs of this container's mask, which has no
+    SMT) feeds whole_host.smt_extrapolated_value, and north_star_ratio quotes
+    the stricter SMT ratio first and decides target_met_whole_host by it."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    aff = sorted(os.sched_getaffinity(0))
+    if len(aff) < 2:
+        pytest.skip("needs two CPUs")
+    monkeypatch.setattr(bench, "smt_pair", lambda: (aff[0], aff[1]))
+    monkeypatch.setattr(bench, "physical_cores", lambda info: 128)
+    recs, _, _ = c_gen_batch(coracle, 0x484B5632, 0, 200, 64, 100, 0)
+    cpu = bench.cpu_baseline([("s", recs, 1, None)], [1, 2], min_s=0.05)
+    wh = cpu["whole_host"]
+    smt = wh["smt_core"]
+    assert smt["cpus"] == [aff[0], aff[1]] and smt["core_rate_smt"] > 0 and smt["core_rate_1t"] > 0
+    assert wh["smt_extrapolated_value"] == round(smt["core_rate_smt"] * 128, 1)
+    assert "UPPER bound" in cpu["kind_note"]
+    assert os.sched_getaffinity(0) == set(aff)  # restored
+    r = bench.north_star_ratio(1e8, cpu)
+    assert list(r)[0] == "whole_host_smt_extrapolated"
+    assert r["whole_host_smt_extrapolated"] == round(1e8 / wh["smt_extrapolated_value"], 1)
+    assert r["target_met_whole_host"] == (r["whole_host_smt_extrapolated"] >= 50.0)
