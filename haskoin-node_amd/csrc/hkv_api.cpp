@@ -71,9 +71,10 @@ struct DevCtx {
   // records, [5] key-check verdict words, [6] host-form verdict words
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t ms_win_cand = 0, ms_win_keys = 0;  // record-window overrides (hkv_debug_ms_window; 0 = default)
   void* ms_ctr = nullptr;            // scan sums: [epoch & 1] this call's (its tail launch zeroes the other)
   // the tail's words: [0..7] and [8..15] the two work-queue slots (claim,
-  // done per phase; launch `tail_epoch` uses slot tail_epoch & 1 and zeroes
+  // completed items; launch `tail_epoch` uses slot tail_epoch & 1 and zeroes
   // the other), [16] the sticky fault latch (hkv_device_fault), [17] the host
   // form's per-call status word
   unsigned int* ms_bar = nullptr;
@@ -146,12 +147,21 @@ size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 #define HKV_SPLIT_DIV 8
 #endif
 
-// verify-std-inputs batches run in chunks of at most STD_CHUNK inputs: the
-// multisig scratch of a chunk is sized by its host bound (136 candidate and
-// 16 key-check records per input: 16-of-16), so the device never reports a
-// count the host must read first; the scan's 32-bit candidate sum cannot wrap
+// verify-std-inputs batches run in chunks of at most STD_CHUNK inputs. The
+// multisig verdict bits of a chunk are sized by the host bound (136 candidate
+// and 16 key-check records per input: 16-of-16), so the device never reports
+// a count the host must read first (the scan's 32-bit candidate sum cannot
+// wrap); the 168-B records themselves live in two windows capped at
+// MS_WIN_CAND + MS_WIN_KEYS records (~512 MiB), through
+// which the tail kernel runs the chunk's records in rounds
 constexpr size_t STD_CHUNK = 1u << 17;
 constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
+#ifndef HKV_MS_WIN_CAND
+#define HKV_MS_WIN_CAND 2752512u  // 43,008 x 64 candidate records (441 MiB)
+#endif
+#ifndef HKV_MS_WIN_KEYS
+#define HKV_MS_WIN_KEYS 442368u   // 6,912 x 64 key-check records (71 MiB)
+#endif
 constexpr size_t HKV_MAX_STD_INPUTS = 0xFFFFFF00ull;
 constexpr size_t MS_BAR_WORDS = 32, MS_FAULT = 16, MS_HOST_STATUS = 17;  // DevCtx::ms_bar
 #ifndef HKV_HOST_FIRST_DIV  // the host-batch path's first chunk: one resident grid / this
@@ -498,13 +508,15 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
 // kernel (hkv_kernels.hip 2e) does the rest, or nothing when the total is 0.
 int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                      uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
-                     const hkv::MsScan& ms, size_t cap_cand);
+                     const hkv::MsScan& ms, size_t cap_cand, size_t cap_keys);
 // the multisig tail's operands for this call (launch epoch d.tail_epoch)
 hkv::MsTail tail_args(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
-                      uint32_t* out_bits, bool fused, const hkv::MsScan& ms, size_t cap_cand) {
+                      uint32_t* out_bits, bool fused, const hkv::MsScan& ms, size_t cap_cand, size_t cap_keys) {
   uint8_t* cand = static_cast<uint8_t*>(d.ms[4]);
   uint64_t* ctr = static_cast<uint64_t*>(d.ms_ctr);
   hkv::MsTail t;
+  t.win_cand = (uint32_t)cap_cand;
+  t.win_keys = (uint32_t)cap_keys;
   t.txs = dt->bytes;
   t.tx_off = dt->offsets;
   t.n_tx = dt->n_tx;
@@ -543,13 +555,19 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
   // the block kernel (at most 16 inputs per CU) runs the multisig scan on
   // its signature wave; otherwise the scan kernel follows the verify launch
   const bool fused_scan = fused && hkv::std_split_scans((uint32_t)round_up(n, hkv::WG), (uint32_t)d.n_cu);
-  const size_t cap_cand = n * MS_CAND_PER_INPUT, cap_keys = n * MS_KEYS_PER_INPUT;
+  const size_t all_cand = n * MS_CAND_PER_INPUT, all_keys = n * MS_KEYS_PER_INPUT;
+  // the record windows: the whole bound when it fits the budget (one round),
+  // else the budget (hkv_debug_ms_window can shrink both for tests)
+  const size_t win_c = d.ms_win_cand ? d.ms_win_cand : HKV_MS_WIN_CAND;
+  const size_t win_k = d.ms_win_keys ? d.ms_win_keys : HKV_MS_WIN_KEYS;
+  const size_t cap_cand = round_up(std::min(all_cand, win_c), 64), cap_keys = round_up(std::min(all_keys, win_k), 64);
   const size_t slots = hkv::ms_tail_slots((uint32_t)d.n_cu);
   int rc = grow(&d.ms[0], &d.ms_cap[0], n * 8, "hipMalloc(multisig desc)");
   if (!rc) rc = grow(&d.ms[2], &d.ms_cap[2], n * 8, "hipMalloc(multisig offsets)");
-  if (!rc) rc = grow(&d.ms[3], &d.ms_cap[3], round_up(cap_cand, 64) / 8, "hipMalloc(multisig candidate bits)");
+  if (!rc) rc = grow(&d.ms[3], &d.ms_cap[3], round_up(all_cand, 64) / 8, "hipMalloc(multisig candidate bits)");
+  // (the key window starts right after this call's candidate window)
   if (!rc) rc = grow(&d.ms[4], &d.ms_cap[4], (cap_cand + cap_keys) * hkv::REC_SIZE, "hipMalloc(multisig records)");
-  if (!rc) rc = grow(&d.ms[5], &d.ms_cap[5], round_up(cap_keys, 64) / 8, "hipMalloc(multisig key bits)");
+  if (!rc) rc = grow(&d.ms[5], &d.ms_cap[5], round_up(all_keys, 64) / 8, "hipMalloc(multisig key bits)");
   // the tail's candidate groups use slot-relative pair-form scratch (grid * 32 signatures)
   if (!rc) rc = ensure_dev_buffers(d, std::max(round_up(n, hkv::WG), round_up(slots, hkv::WG)));
   if (!rc) rc = ensure_aux(d, std::max(round_up(n, hkv::WG), round_up(slots, hkv::WG)), st);
@@ -612,7 +630,8 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
     rc = enqueue_std_inputs(d, dt, jobs, n, forkid, recs, st);
   }
   if (!rc)
-    rc = enqueue_std_rest(d, dt, jobs, n, forkid, recs, out_bits, st, fused, fused_scan, overlap, ms, cap_cand);
+    rc = enqueue_std_rest(d, dt, jobs, n, forkid, recs, out_bits, st, fused, fused_scan, overlap, ms, cap_cand,
+                          cap_keys);
   // a failed call still orders st after the hash half (the next call's
   // scratch acquire then waits for it too)
   if (rc && forked) (void)hipStreamWaitEvent(st, d.ev_join, 0);
@@ -624,7 +643,7 @@ int enqueue_std_chunk(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, s
 // multisig scan, the record verify, the multisig tail
 int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid, void* recs,
                      uint32_t* out_bits, hipStream_t st, bool fused, bool fused_scan, bool overlap,
-                     const hkv::MsScan& ms, size_t cap_cand) {
+                     const hkv::MsScan& ms, size_t cap_cand, size_t cap_keys) {
   int rc = HKV_OK;
   if (!fused_scan && !overlap)  // (the overlapped form scanned on the hash stream)
     HKV_TRY(hkv::launch_ms_scan(dt->bytes, dt->n_tx, d.txt, dt->scripts, dt->scripts_len, jobs, (uint32_t)n, forkid,
@@ -641,7 +660,8 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
   // by n_cu, hkv_internal.h launch_ms_tail; a smaller grid for block-sized
   // batches measured no different, profiles/r05k/tail_grid_ab.txt)
   const uint32_t tail_grid = (uint32_t)d.n_cu;
-  HKV_TRY(hkv::launch_ms_tail(tail_args(d, dt, jobs, n, forkid, out_bits, fused, ms, cap_cand), tail_grid, st),
+  HKV_TRY(hkv::launch_ms_tail(tail_args(d, dt, jobs, n, forkid, out_bits, fused, ms, cap_cand, cap_keys), tail_grid,
+                              st),
           "multisig tail launch");
   ++d.tail_epoch;  // (launched: it zeroes the slot and the scan sum the next call uses)
   d.inject_tail = false;
@@ -776,6 +796,24 @@ int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (when == HKV_FAIL_TAIL) ctx->devs[(size_t)dev].inject_tail = true;
   else ctx->devs[(size_t)dev].inject = when;
+  return HKV_OK;
+}
+
+int hkv_debug_ms_window(hkv_ctx* ctx, int dev, uint32_t cand_records, uint32_t key_records) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || cand_records > HKV_MS_WIN_CAND ||
+      key_records > HKV_MS_WIN_KEYS)
+    return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DevCtx& d = ctx->devs[(size_t)dev];
+  d.ms_win_cand = (uint32_t)round_up(cand_records, 64);
+  d.ms_win_keys = (uint32_t)round_up(key_records, 64);
+  return HKV_OK;
+}
+
+int hkv_debug_ms_scratch(hkv_ctx* ctx, int dev, size_t* bytes) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !bytes) return HKV_E_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  *bytes = ctx->devs[(size_t)dev].ms_cap[4];
   return HKV_OK;
 }
 

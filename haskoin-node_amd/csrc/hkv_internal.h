@@ -61,16 +61,18 @@ struct MsTail {
   const uint64_t* off;
   unsigned long long* total;        // this call's scan sum (MsScan counters: ms_ctr[epoch & 1])
   unsigned long long* total_next;   // the next call's (ms_ctr[(epoch + 1) & 1]): zeroed by this launch
-  uint8_t* cand;                    // candidate records (capacity n * 136)
-  uint8_t* keyrec;                  // key-check records (capacity n * 16)
-  uint32_t* cbits;                  // candidate verdict words
-  uint32_t* kbits;                  // key-check verdict words
+  uint8_t* cand;                    // the candidate record window (win_cand records)
+  uint8_t* keyrec;                  // the key-check record window (win_keys records)
+  uint32_t win_cand, win_keys;      // window capacities in records (multiples of 64): the tail runs
+                                    // ceil(count / window) rounds of emit + verify
+  uint32_t* cbits;                  // candidate verdict words (every candidate of the chunk)
+  uint32_t* kbits;                  // key-check verdict words (every key check of the chunk)
   uint32_t* im;                     // pair-form scratch: slot stride = grid * 32
   uint32_t* aux;
   const uint32_t* gtab;
   uint32_t* qs;
   uint32_t* out_bits;               // the batch's verdict words (multisig inputs are ORed in)
-  unsigned int* bar;                // two work-queue slots of 8 words (claim, done[4]): launch `epoch` uses
+  unsigned int* bar;                // two work-queue slots of 8 words (claim, done): launch `epoch` uses
                                     // slot epoch & 1 and zeroes the other
   uint32_t epoch;                   // this launch's sequence number on the device
   unsigned int* fault;              // the device's sticky fault latch (hkv_device_fault)

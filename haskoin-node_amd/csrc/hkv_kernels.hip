@@ -197,13 +197,16 @@ __global__ void __launch_bounds__(WG, HKV_PROLOGUE_WAVES) hkv_prologue_kernel(co
 // every key with importPubKey, so one key off the curve fails the input
 // whatever its signatures do): bit i = record i's key parses. Bits leave as
 // one 64-bit ballot word per wave (i's wave covers 64 consecutive records).
-HKV_DEV void key_check_lane(const uint32_t* __restrict__ recs, uint32_t i, uint32_t n, uint32_t* __restrict__ bits) {
+// recs holds records [rbase, ...): record i is read at recs[i - rbase] (the
+// multisig tail's key-check window; rbase a multiple of 64).
+HKV_DEV void key_check_lane(const uint32_t* __restrict__ recs, uint32_t i, uint32_t n, uint32_t* __restrict__ bits,
+                            uint32_t rbase = 0) {
   uint32_t w[REC_WORDS];
 #pragma unroll
   for (int k = 0; k < REC_WORDS; ++k) w[k] = 0;
   if (i < n) {
 #pragma unroll
-    for (int k = 24; k < 42; ++k) w[k] = recs[(size_t)i * REC_WORDS + k];
+    for (int k = 24; k < 42; ++k) w[k] = recs[(size_t)(i - rbase) * REC_WORDS + k];
   }
   fe x, y;
   const bool ok = pubkey_parse_rec(w, x, y) && i < n;
@@ -862,7 +865,13 @@ HKV_DEV void pair_chain(fe& P, fe& Z, bool& inf, const QLane& ql, const uint32_t
   inf = true;
   fe_set_zero(P);
   fe_set_zero(Z);
-  auto digit = [&](uint32_t w) { return half ? (int)((w >> QDIG_BITS) & QDIG_MASK) - QBIAS : (int)(w & QDIG_MASK) - QBIAS; };
+  // the half's digit and the odd lane's negation as VGPR arithmetic (a shift
+  // count, a mask), so no lane-mask SGPR pair is live through the windows:
+  // two such pairs were lane-spilled and reloaded (4 v_readlane) in every
+  // window
+  const uint32_t dshift = half ? QDIG_BITS : 0u;
+  const uint32_t negm = negh ? odd : 0u;  // the GLV half's sign on the odd (y) lane
+  auto digit = [&](uint32_t w) { return (int)((w >> dshift) & QDIG_MASK) - QBIAS; };
   uint32_t dw = valid ? im[(size_t)(IM_DIG + w_hi) * n_pad + i] : DIG_ZERO;
   bool dbl = false;  // the first window starts from infinity: no doublings
 #if HKV_TOP_MERGE
@@ -882,12 +891,12 @@ HKV_DEV void pair_chain(fe& P, fe& Z, bool& inf, const QLane& ql, const uint32_t
       fe T;
 #pragma unroll
       for (int k = 0; k < 8; ++k) T.v[k] = ql[e1 ? e1 - 1 : 0][k][ln];
-      fe_cneg(T, T, negh && odd);
+      fe_cneg_mask(T, T, negm);
       pair_accumulate_from_inf(P, Z, inf, T, e1 != 0);
       if (__any(e2 != 0)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) T.v[k] = ql[e2 ? e2 - 1 : 0][k][ln];
-        fe_cneg(T, T, negh && odd);
+        fe_cneg_mask(T, T, negm);
         pair_accumulate(P, Z, inf, T, e2 != 0, odd);  // T[8] + T[8] (m = 16): its exact doubling
       }
       w_hi -= 2;
@@ -910,11 +919,10 @@ HKV_DEV void pair_chain(fe& P, fe& Z, bool& inf, const QLane& ql, const uint32_t
     }
     dbl = true;
     const bool take = dg != 0;
-    const bool neg = (dg < 0) != negh;
     fe T;
 #pragma unroll
     for (int k = 0; k < 8; ++k) T.v[k] = ql[ie][k][ln];
-    fe_cneg(T, T, neg && odd);  // y -> -y on the odd lane
+    fe_cneg_mask(T, T, ((uint32_t)(dg >> 31) & odd) ^ negm);  // y -> -y on the odd lane: (dg < 0) != negh
     const bool was_inf = inf;
     pair_accumulate(P, Z, inf, T, take, odd);
     if (__any(take && was_inf)) pair_accumulate_from_inf(P, Z, inf, T, take && was_inf);
@@ -2552,22 +2560,34 @@ namespace hkv {
 //     then phase 3's key-check chunks and candidate groups, then phase 4's
 //     walk chunks) are claimed in that order by a device counter, and a
 //     workgroup starts an item only once every item of the phase before has
-//     completed. A workgroup waits only when no earlier item is left to
-//     claim, i.e. for items other workgroups are running — so progress never
-//     depends on a workgroup that is not resident, and the launch needs no
-//     co-residency (a cooperative launch, which guarantees it, cost ~23 us
-//     per call on the block path: profiles/r05a/coop_ab.txt). The wait is
-//     bounded anyway (~seconds, far above one item): a workgroup that gives
-//     up leaves the verdicts it owns at 0 (reject, never a false accept) and
-//     reports HKV_STATUS_TAIL_FAULT through the device's sticky latch and the
-//     call's status word. Each call counts in its own queue slot and scan
-//     sum (the parity of its tail epoch) and its tail zeroes the other pair
-//     for the next call, so nothing a faulted launch leaves behind reaches a
-//     later one. (The tail inside the block kernel instead — groups claimed
-//     from the queue, the tail's items after them — saved this launch but
-//     cost ~15 us per block: profiles/r05e/fused_tail_ab.txt.)
+//     completed (one running count of completed items: since no item starts
+//     before the phase before it has completed, "count >= the phase's first
+//     item index" says exactly that). A workgroup waits only when no earlier
+//     item is left to claim, i.e. for items other workgroups are running — so
+//     progress never depends on a workgroup that is not resident, and the
+//     launch needs no co-residency (a cooperative launch, which guarantees
+//     it, cost ~23 us per call on the block path: profiles/r05a/coop_ab.txt).
+//     The wait is bounded anyway (~seconds, far above one item): a workgroup
+//     that gives up leaves the verdicts it owns at 0 (reject, never a false
+//     accept) and reports HKV_STATUS_TAIL_FAULT through the device's sticky
+//     latch and the call's status word. Each call counts in its own queue
+//     slot and scan sum (the parity of its tail epoch) and its tail zeroes
+//     the other pair for the next call, so nothing a faulted launch leaves
+//     behind reaches a later one. (The tail inside the block kernel instead —
+//     groups claimed from the queue, the tail's items after them — saved this
+//     launch but cost ~15 us per block: profiles/r05e/fused_tail_ab.txt.)
+//
+//     Records in rounds: the candidate and key-check records live in two
+//     fixed windows (win_cand / win_keys records, host-sized to a budget,
+//     hkv_api.cpp MS_WIN_*), not in buffers sized by the 16-of-16 bound, so
+//     phases 2 and 3 run once per round r over records
+//     [r * win, (r + 1) * win) of the scan's allocation: the emit writes
+//     only the records in the round's windows (hashing only the signatures
+//     with one there), the verifies read them and write their verdict bits
+//     at the global index. Phase 4 reads every round's bits.
 // ---------------------------------------------------------------------------
-enum : uint32_t { TQ_CLAIM = 0, TQ_DONE = 1, TQ_SLOT = 8 };  // slot words: claim, done[4]
+// ---------------------------------------------------------------------------
+enum : uint32_t { TQ_CLAIM = 0, TQ_DONE = 1, TQ_SLOT = 8 };  // slot words: claim, done (completed items)
 // wait (thread 0) until `done` reaches `want`; false on a timeout (fault reported).
 // The test hook (force_fault) gives up at every phase transition without
 // looking at the count: a launch with any multisig input has items of at
@@ -2615,25 +2635,33 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
   const uint32_t n_cand = (uint32_t)total, n_keys = (uint32_t)(total >> 32);
   if (n_keys == 0) return;  // no multisig input (every input has >= 1 key): uniform over the grid
   const uint32_t T = PAIR_TPB;
+  const uint32_t Wc = a.win_cand, Wk = a.win_keys;  // (multiples of 64, >= 64)
+  const uint32_t rounds = max((n_cand + Wc - 1) / Wc, (n_keys + Wk - 1) / Wk);
+  const uint32_t wc = min(Wc, n_cand), wk = min(Wk, n_keys);  // records per (full) round
   const uint32_t n1 = (a.hash_txs != TX_HASHES_NONE) ? (3 * a.n_tx + T - 1) / T : 0;  // hash chunks
   const uint32_t n2 = (a.n + T - 1) / T;                                                // record chunks
-  const uint32_t n3k = (n_keys + T - 1) / T, n3 = n3k + (n_cand + PAIR_SIGS - 1) / PAIR_SIGS;
-  const uint32_t n4 = n2;                                                               // walk chunks
-  const uint32_t e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4;
+  const uint32_t n3k = (wk + T - 1) / T, n3 = n3k + (wc + PAIR_SIGS - 1) / PAIR_SIGS;  // per round
+  const uint32_t per = n2 + n3;
+  const uint32_t e1 = n1, e3 = e1 + rounds * per, e4 = e3 + n2;
   const uint32_t slots = gridDim.x * PAIR_SIGS, sbase = blockIdx.x * PAIR_SIGS;
   const StdArgs none{};
-  int seen = 0;  // phases known complete (this workgroup's view)
+  uint32_t seen = 0;  // the first item index of the latest phase known complete before it (this workgroup's view)
   for (;;) {
     if (threadIdx.x == 0) {
       const uint32_t it = atomicAdd(&q[TQ_CLAIM], 1u);
-      const int ph = it < e1 ? 0 : (it < e2 ? 1 : (it < e3 ? 2 : 3));
       uint32_t ok = it < e4 ? 1u : 0u;
-      // the phase before this item's must be complete (items are claimed in
-      // phase order, so only running items can be outstanding)
-      const uint32_t need[4] = {0u, n1, n2, n3};
-      if (ok && ph > seen) {
-        ok = tail_wait(a, &q[TQ_DONE + ph - 1], need[ph]) ? 1u : 0u;
-        if (ok) seen = ph;
+      // the first item of this item's phase: every item before it must have
+      // completed (items are claimed in phase order, so only running items
+      // can be outstanding)
+      uint32_t start = 0;
+      if (it >= e3) start = e3;
+      else if (it >= e1) {
+        const uint32_t r0 = e1 + (it - e1) / per * per;
+        start = it - r0 < n2 ? r0 : r0 + n2;
+      }
+      if (ok && start > seen) {
+        ok = tail_wait(a, &q[TQ_DONE], start) ? 1u : 0u;
+        if (ok) seen = start;
       }
       item_s = it;
       go_s = ok;
@@ -2642,7 +2670,6 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
     const uint32_t it = item_s, go = go_s;
     __syncthreads();
     if (!go) return;
-    int ph;
     if (it < e1) {
       // 1. the BIP143 per-tx hashes (lanes hash-major, so a wave mostly
       //    shares its hash). Every tx of the batch is hashed, and the block
@@ -2650,7 +2677,6 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
       //    block's coinbase has none), so each lane re-derives its tx's row
       //    from the offsets — a stale row of an earlier call would point the
       //    hash outside the tx — and writes back only the hash words.
-      ph = 0;
       const uint32_t x = it * T + threadIdx.x;
       bool go1 = x < 3 * a.n_tx;
       const uint32_t t = go1 ? x % a.n_tx : 0, which = go1 ? x / a.n_tx : 0;
@@ -2658,44 +2684,48 @@ __global__ void __launch_bounds__(PAIR_TPB, 1) hkv_ms_tail_kernel(MsTail a) {
       if (go1) tx_index_row(a.txs, a.tx_off, t, row);
       if (go1 && a.hash_txs == TX_HASHES_WITNESS) go1 = (row[TXT_FLAGS] & TXF_WITNESS) != 0;
       tx_hash_word_lane(a.txs, row, a.txt + (size_t)t * TXT_WORDS, which, go1, buf);
-    } else if (it < e2) {
-      // 2. key-check and candidate records
-      ph = 1;
-      const uint32_t jx = (it - e1) * T + threadIdx.x;
-      ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
-                   a.cand, a.keyrec, buf);
     } else if (it < e3) {
-      // 3. a chunk of key checks, or a pair-form group of 32 candidates on
-      //    this workgroup's own scratch slots
-      ph = 2;
-      const uint32_t k = it - e2;
-      if (k < n3k) {
-        key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), k * T + threadIdx.x, n_keys, a.kbits);
+      const uint32_t r = (it - e1) / per, k0 = (it - e1) % per;
+      const uint32_t cw0 = r * Wc, kw0 = r * Wk;  // the round's windows (global record indices)
+      if (k0 < n2) {
+        // 2. key-check and candidate records of the round's windows
+        const uint32_t jx = k0 * T + threadIdx.x;
+        ms_emit_lane(a.txs, a.n_tx, a.txt, a.scripts, a.scripts_len, a.jobs, jx, jx < a.n, a.forkid, a.desc, a.off,
+                     a.cand, a.keyrec, cw0, Wc, kw0, Wk, buf);
+      } else if (k0 - n2 < n3k) {
+        // 3a. a chunk of the round's key checks (bits at the global index)
+        const uint32_t i = kw0 + (k0 - n2) * T + threadIdx.x;
+        key_check_lane(reinterpret_cast<const uint32_t*>(a.keyrec), i, min(n_keys, kw0 + Wk), a.kbits, kw0);
       } else {
-        // the group's records [base, base + 32) run on this workgroup's own
-        // scratch slots [sbase, sbase + 32): pair_group indexes records and
-        // verdict words by slot, so both are handed over shifted by
-        // base - sbase, which is negative when the group lies below the slot
-        // (a queue hands any group to any workgroup) — formed on the 64-bit
-        // address as an integer, never as an out-of-range pointer, and every
-        // access lands at base + lane >= 0
-        const uint32_t base = (k - n3k) * PAIR_SIGS;
+        // 3b. a pair-form group of 32 of the round's candidates on this
+        //     workgroup's own scratch slots [sbase, sbase + 32): pair_group
+        //     indexes records and verdict words by slot, so both are handed
+        //     over shifted — the verdict words by base - sbase (base = the
+        //     group's global index), the records by base - cw0 - sbase (their
+        //     place in the window) — which is negative when the group lies
+        //     below the slot (a queue hands any group to any workgroup):
+        //     formed on the 64-bit address as an integer, never as an
+        //     out-of-range pointer, and every access lands at a record and a
+        //     verdict word of the group
+        const uint32_t base = cw0 + (k0 - n2 - n3k) * PAIR_SIGS;
         const int64_t shift = (int64_t)base - (int64_t)sbase;  // a multiple of 32
+        const int64_t rshift = shift - (int64_t)cw0;
         uint32_t* recs = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(a.cand) +
-                                                     (uintptr_t)(shift * (int64_t)(REC_WORDS * 4)));
+                                                     (uintptr_t)(rshift * (int64_t)(REC_WORDS * 4)));
         uint32_t* bits = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(a.cbits) +
                                                      (uintptr_t)(shift / 32 * 4));
-        // slot i is record i + shift: valid iff i + shift < n_cand (mod 2^32: n_cand - shift < 2^32)
-        pair_group<false>(sbase, a.im, (uint32_t)((int64_t)n_cand - shift), slots, a.gtab, bits, 0xFFFFFFFFu, a.aux,
+        // slot i is record i + shift: valid iff i + shift < the round's end
+        // (mod 2^32: end - shift < 2^32)
+        const uint32_t end = min(n_cand, cw0 + Wc);
+        pair_group<false>(sbase, a.im, (uint32_t)((int64_t)end - shift), slots, a.gtab, bits, 0xFFFFFFFFu, a.aux,
                           recs, HKV_MODE_HASKOIN, nullptr, none, qlds, hlds, xch, buf);
       }
     } else {
       // 4. the countMulSig walk
-      ph = 3;
       const uint32_t jx = (it - e3) * T + threadIdx.x;
       ms_resolve_lane(a.desc, a.off, jx, jx < a.n, a.cbits, a.kbits, a.out_bits);
     }
-    publish_count(&q[TQ_DONE + ph]);
+    publish_count(&q[TQ_DONE]);
   }
 }
 

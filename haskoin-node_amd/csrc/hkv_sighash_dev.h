@@ -1394,13 +1394,19 @@ HKV_DEV void ms_write_record(uint32_t* r32, const uint32_t msg[8], const uint32_
 // The records of one scanned multisig input (the tail kernel's emit phase):
 // one key-check record per key of its script (msg, r, s zero), then per
 // signature j < s_eff its sighash and the candidate records (msg_j, r_j, s_j,
-// key_k), k = j..n-1, at the ranges the scan allocated. Block-synchronous
-// hashing: call from wave-uniform control flow with buf = 16 * blockDim words.
+// key_k), k = j..n-1, at the ranges the scan allocated. Only the records that
+// fall in this round's windows are written — candidate records
+// [cw0, cw0 + cwn) at cand[index - cw0], key-check records [kw0, kw0 + kwn)
+// at keyrec[index - kw0] — and a signature none of whose candidates falls
+// in the window is not hashed (the tail runs its record windows in rounds so
+// that its scratch stays within a fixed budget). Block-synchronous hashing:
+// call from wave-uniform control flow with buf = 16 * blockDim words.
 HKV_DEV void ms_emit_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const uint32_t* __restrict__ txt,
                           const uint8_t* __restrict__ scripts, uint32_t scripts_len,
                           const hkv_input_job* __restrict__ jobs, uint32_t jx, bool in_range, int32_t forkid,
                           const uint32_t* __restrict__ desc, const uint64_t* __restrict__ off64,
-                          uint8_t* __restrict__ cand, uint8_t* __restrict__ keyrec, uint32_t* buf) {
+                          uint8_t* __restrict__ cand, uint8_t* __restrict__ keyrec, uint32_t cw0, uint32_t cwn,
+                          uint32_t kw0, uint32_t kwn, uint32_t* buf) {
   bool go = in_range && (desc[2 * (size_t)jx] & MS_OK);
   MsIn r;
   r.code = r.rd = r.wprog = scripts; r.code_len = r.rd_len = 0; r.s_eff = 0; r.mask = 0; r.n = 0;
@@ -1423,9 +1429,11 @@ HKV_DEV void ms_emit_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const 
   if (go) {
     const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t k = 0; k < r.n; ++k) {
+      const uint32_t w = kbase + k - kw0;  // (wraps past 2^32 below the window)
+      if (w >= kwn) continue;
       uint32_t kl;
       const uint8_t* kp = ms_key(r.code, k, kl);
-      ms_write_record(reinterpret_cast<uint32_t*>(keyrec + (size_t)(kbase + k) * REC_SIZE), z, z, z, kp, kl);
+      ms_write_record(reinterpret_cast<uint32_t*>(keyrec + (size_t)w * REC_SIZE), z, z, z, kp, kl);
     }
   }
   uint32_t off = r.it_off, idx = cbase;
@@ -1435,7 +1443,10 @@ HKV_DEV void ms_emit_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const 
     const bool here = go && j < r.s_eff;
     uint32_t d_off = 0, d_len = 0;
     if (here) (void)ms_item(txs, r, off, d_off, d_len);
-    const bool live = here && ((r.mask >> j) & 1u);
+    // signature j's candidates [idx, idx + n - j) against the window: the
+    // hash is needed only when one of them is written in this round
+    const uint32_t lo = idx > cw0 ? idx : cw0, hi_w = cw0 + cwn, hi_j = idx + (r.n - j);
+    const bool live = here && ((r.mask >> j) & 1u) && lo < (hi_w < hi_j ? hi_w : hi_j);
     uint32_t rr[8], ss[8], sh = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) rr[k] = ss[k] = 0;
@@ -1443,7 +1454,9 @@ HKV_DEV void ms_emit_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const 
     JobCtx c;
     c.forkid_form = false; c.one = false; c.single_hash = false;
     if (live) job_setup(c, txs, row, input, sh, r.wit, forkid);  // P2WSH: BIP143 over the witness script
-    uint32_t* r32 = reinterpret_cast<uint32_t*>(cand + (size_t)idx * REC_SIZE);  // first record of sig j
+    // (scratch for hashOutputs: the first of sig j's records in the window,
+    // overwritten by that record once the hash is done)
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(cand + (size_t)(live ? lo - cw0 : 0u) * REC_SIZE);
     const bool need_single = live && c.single_hash;
     if (__any(need_single)) {
       gen_clear(g);
@@ -1465,11 +1478,14 @@ HKV_DEV void ms_emit_lane(const uint8_t* __restrict__ txs, uint32_t n_tx, const 
 #pragma unroll
       for (int k = 0; k < 8; ++k) msg[k] = hashed ? d[k] : (k == 0 ? 1u : 0u);
       for (uint32_t k = j; k < r.n; ++k) {
+        const uint32_t w = idx + (k - j) - cw0;  // (wraps past 2^32 below the window)
+        if (w >= cwn) continue;
         uint32_t kl;
         const uint8_t* kp = ms_key(r.code, k, kl);
-        ms_write_record(reinterpret_cast<uint32_t*>(cand + (size_t)(idx++) * REC_SIZE), msg, rr, ss, kp, kl);
+        ms_write_record(reinterpret_cast<uint32_t*>(cand + (size_t)w * REC_SIZE), msg, rr, ss, kp, kl);
       }
     }
+    if (here && ((r.mask >> j) & 1u)) idx += r.n - j;
   }
 }
 

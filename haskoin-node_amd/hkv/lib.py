@@ -71,6 +71,8 @@ EXPORTS = {
     "hkv_device_failures": (c_int, [c_void_p, c_int]),
     "hkv_device_reset_health": (c_int, [c_void_p, c_int]),
     "hkv_debug_fail_device": (c_int, [c_void_p, c_int, c_uint32]),
+    "hkv_debug_ms_window": (c_int, [c_void_p, c_int, c_uint32, c_uint32]),
+    "hkv_debug_ms_scratch": (c_int, [c_void_p, c_int, POINTER(c_size_t)]),
     "hkv_batch_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "hkv_batch_free": (None, [c_void_p]),
     "hkv_batch_records": (POINTER(c_uint8), [c_void_p]),

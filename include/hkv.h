@@ -122,6 +122,14 @@ int hkv_device_failures(hkv_ctx* ctx, int dev);
  * multisig input. */
 #define HKV_FAIL_TAIL 4u
 int hkv_debug_fail_device(hkv_ctx* ctx, int dev, uint32_t when);
+/* Test hooks of the multisig record windows (hkv_verify_std_inputs*): the
+ * tail runs a chunk's candidate and key-check records in rounds through two
+ * windows of at most 2,752,512 + 442,368 records (~512 MiB); _window sets
+ * smaller capacities for device dev's later calls (records, rounded up to
+ * 64; 0 = the default), so tests can force many rounds on small batches;
+ * _scratch reports the bytes the windows hold allocated on device dev. */
+int hkv_debug_ms_window(hkv_ctx* ctx, int dev, uint32_t cand_records, uint32_t key_records);
+int hkv_debug_ms_scratch(hkv_ctx* ctx, int dev, size_t* bytes);
 
 /* Pinned host record buffer with room for max_n records. */
 int hkv_batch_alloc(hkv_ctx* ctx, size_t max_n, hkv_batch** out);
@@ -254,10 +262,12 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * and does nothing when it is 0), so a
  * caller may enqueue block k+1 while block k verifies, and hip_stream may be
  * gated on events recorded after the call. Batches run in chunks of 131,072
- * inputs (the multisig scratch is sized per chunk by its 16-of-16 bound, 136
- * candidate + 16 key-check records per input, allocated on first use).
- * Scratch footprint: (136 + 16) * 168 B per input of the largest chunk seen,
- * i.e. ~0.1 GB for a 4,000-input block, ~3.35 GB for a full 131,072 chunk.
+ * inputs. Multisig scratch per chunk: the verdict bits by the 16-of-16 bound
+ * (136 candidate + 16 key-check bits per input) and the 168-B records in two
+ * windows, the bound or at most 2,752,512 + 442,368 records (~512 MiB), which
+ * the tail runs in rounds when a chunk's records exceed them: ~0.1 GB for a
+ * 4,000-input block, ~512 MiB for any larger chunk, multisig or not,
+ * allocated on first use and kept.
  * A multisig tail whose work-queue wait gave up leaves its multisig
  * verdicts at 0 and reports HKV_STATUS_TAIL_FAULT (below) — this form only
  * through hkv_device_fault; use the _status form to get it per call.

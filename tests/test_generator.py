@@ -54,3 +54,17 @@ def test_uncompressed_share_and_negated_keys(coracle):
     assert set(np.unique(r[~unc, 97])) <= {2, 3} and (r[unc, 97] == 4).all()
     neg = cls == 4
     assert neg.any() and not lab[neg].any()
+
+
+def test_blockgen_ripemd160_published_vectors():
+    """hkv.blockgen's RIPEMD-160 (the multisig generator's P2SH hashes)
+    against the published test vectors and the oracle's restatement."""
+    import os
+    import sighash_oracle as sh
+    from hkv.blockgen import ripemd160
+    assert ripemd160(b"").hex() == "9c1185a5c5e9fc54612808977ee8f548b2258d31"
+    assert ripemd160(b"abc").hex() == "8eb208f7e05d987a9b044a8e98c6b087f15a0bfc"
+    assert ripemd160(b"message digest").hex() == "5d0689ef49d2fae572b881b123a85ffa21595f36"
+    for n in (55, 56, 64, 119, 120, 300):
+        d = os.urandom(n)
+        assert ripemd160(d) == sh.ripemd160(d)

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TAG=${TAG:-ablib}
 B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-adversarial --no-headers --no-merkle --no-host-path"
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 \
+timeout -k 10 ${PYTEST_LIMIT:-900} python -u -m pytest tests -x -v -m gpu --timeout 800 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 \
   && echo "pytest ok" && tail -1 gpurun_out/${TAG}_pytest.log || exit 1
 for k in 1 2; do
   HKV_LIB=haskoin-node_amd/lib/libhkv_base.so timeout -k 10 200 python $B > gpurun_out/${TAG}_base$k.log 2>&1 || exit 1
