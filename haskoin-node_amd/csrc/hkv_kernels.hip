@@ -545,6 +545,13 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
                                                                                  StdArgs sa) {
   const uint32_t n_lanes = gridDim.x * WG;
   const uint32_t lane = blockIdx.x * WG + threadIdx.x;
+#if HKV_ECMULT_PARK
+  // per-lane LDS slots for state the chain does not touch (the table scale
+  // Zg, used only after the last window) and the GLV signs the accumulate
+  // reads once per term: at 4 waves per SIMD (128 VGPRs) these were spilled
+  // to scratch; LDS is idle in this kernel (9 KiB per workgroup)
+  __shared__ uint32_t park[9][WG];
+#endif
   // optional clock probe (hkv_profile_clock): shader-clock and constant-rate
   // counters around block 0's work, so bench.py prices the roofline at the
   // clock the launch actually ran at
@@ -603,6 +610,11 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
         qtab_store(qs, n_lanes, lane, (j - 1), 4, h);
       }
       fe_mul(Zg, p2.z, pj.z);  // total scale: phi_Z2 then phi_Zc, Zc = pj.z
+#if HKV_ECMULT_PARK
+#pragma unroll
+      for (int k = 0; k < 8; ++k) park[k][threadIdx.x] = Zg.v[k];
+      park[8][threadIdx.x] = (neg1 ? 1u : 0u) | (neg2 ? 2u : 0u);
+#endif
       fe beta;
 #pragma unroll
       for (int k = 0; k < 8; ++k) beta.v[k] = FE_BETA[k];
@@ -684,7 +696,11 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
         if (t >= 2 && !__any(take)) continue;
         const int mg = dg < 0 ? -dg : dg;
         const int ie = mg ? mg - 1 : 0;
+#if HKV_ECMULT_PARK
+        const bool neg = (dg < 0) != (((park[8][threadIdx.x] >> slot) & 1u) != 0);
+#else
         const bool neg = (dg < 0) != (slot == 0 ? neg1 : neg2);
+#endif
         fe tx, ty;
         qtab_load(qs, n_lanes, lane, ie, (slot == 0 ? 0 : 4), tx);
         qtab_load(qs, n_lanes, lane, ie, 2, ty);
@@ -701,6 +717,10 @@ __global__ void __launch_bounds__(WG, ILP ? 2 : HKV_ECMULT_WAVES) hkv_ecmult_ker
 
     // hand B' = (X, Y, Z acc * Zg) on E_w to the finish kernel
     fe zt;
+#if HKV_ECMULT_PARK
+#pragma unroll
+    for (int k = 0; k < 8; ++k) Zg.v[k] = park[k][threadIdx.x];
+#endif
     fe_mul(zt, acc.z, Zg);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

@@ -136,6 +136,9 @@ constexpr uint32_t TXF_OK = 1u, TXF_WITNESS = 2u;
 enum : uint32_t { TX_HASHES_NONE = 0, TX_HASHES_ALL = 1, TX_HASHES_WITNESS = 2 };
 
 // minimum waves per SIMD the ecmult kernel's register allocation targets
+#ifndef HKV_ECMULT_PARK  // hkv_ecmult_kernel parks Zg and the GLV signs in LDS (1) or leaves them to the allocator (0)
+#define HKV_ECMULT_PARK 1
+#endif
 #ifndef HKV_ECMULT_WAVES
 #define HKV_ECMULT_WAVES 4
 #endif
