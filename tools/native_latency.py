@@ -1,8 +1,9 @@
-"""Block files for tools/native_latency.cpp: BASELINE configs[0] (or the
-configs[2] block mix) as the tx bytes, the n_tx + 1 offsets, the script
-pool and the hkv_input_job array, in the layouts include/hkv.h defines.
+"""Block files for tools/native_latency.cpp and tools/native_concurrency.cpp:
+BASELINE configs[0] (or the configs[2] block mix, or a 600-tx multisig block)
+as the tx bytes, the n_tx + 1 offsets, the script pool and the hkv_input_job
+array, in the layouts include/hkv.h defines.
 
-    python3 tools/native_latency.py dump gpurun_out/blk0 [config0|config2]
+    python3 tools/native_latency.py dump gpurun_out/blk0 [config0|config2|multisig]
 """
 import os
 import sys
@@ -19,7 +20,12 @@ def dump(out_dir: str, which: str = "config0") -> None:
     from hkv.sighash import INPUT_JOB_DTYPE, TxBatch
     os.makedirs(out_dir, exist_ok=True)
     with hkv.Verifier(hkv.VerifierConfig(device_ids=[0], flags=1)) as v:
-        txs, inputs = blockgen.make_p2pkh_block(v, torch) if which == "config0" else blockgen.make_block(v, torch)
+        if which == "config0":
+            txs, inputs = blockgen.make_p2pkh_block(v, torch)
+        elif which == "multisig":
+            txs, inputs = blockgen.make_multisig_block(v, torch, n_tx=600)
+        else:
+            txs, inputs = blockgen.make_block(v, torch)
     tb = TxBatch(txs)
     jobs = np.zeros(len(inputs), dtype=INPUT_JOB_DTYPE)
     for k, (t, i, spk, value) in enumerate(inputs):
