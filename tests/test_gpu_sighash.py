@@ -991,8 +991,14 @@ def test_multisig_block_stress(torch, ver, coracle):
     multisig case of txgen (bare / P2SH / P2WSH / P2SH-P2WSH, m-of-n, wrong
     order, bad keys, NULLDUMMY), fork id alternating: device-form verdicts
     (and every fifth batch the host form) equal the oracle's on every input,
-    and no call reports a tail fault."""
+    and no call reports a tail fault. HKV_STRESS_MS_WINDOW=c,k runs every
+    batch with the tail's record windows forced to c candidate / k key-check
+    records (hkv_debug_ms_window: many rounds per batch)."""
     import hkv
+    win = os.environ.get("HKV_STRESS_MS_WINDOW")
+    if win:
+        c, kk = (int(x) for x in win.split(","))
+        assert ver.lib.hkv_debug_ms_window(ver.ctx, 0, c, kk) == 0
     for k in range(int(os.environ["HKV_STRESS_MS_BLOCKS"])):
         forkid = None if k % 2 == 0 else 0
         raw, jobs, labels = _ms_block(random.Random(0x4D530000 + k), forkid)
@@ -1003,4 +1009,6 @@ def test_multisig_block_stress(torch, ver, coracle):
         if k % 5 == 0:
             assert hkv.verify_std_inputs(ver, raw, jobs, forkid) == want, k
         print(f"multisig block stress: {k + 1} batches ({len(jobs)} inputs) match", flush=True)
+    if win:
+        assert ver.lib.hkv_debug_ms_window(ver.ctx, 0, 0, 0) == 0
     assert ver.device_fault(0) == 0

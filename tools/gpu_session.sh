@@ -15,7 +15,9 @@
 #                                      caller, configs[4] at the N > 1 shard sizes,
 #                                      a 120-s sustained 1M run
 #   tools/gpu_session.sh stress TAG    the opt-in stress tests (record / wire
-#                                      mutations, multisig blocks, overlapping callers)
+#                                      mutations, multisig blocks — also with the
+#                                      tail's record windows forced small —,
+#                                      overlapping callers)
 #
 # Same-box A/Bs against haskoin-node_amd/lib/libhkv_base.so: tools/gpu_ab_lib.sh
 # (block legs) and tools/gpu_ab_1m.sh (the 1M headline + traffic).
@@ -88,6 +90,8 @@ stress)
       > ${O}_wire.log 2>&1 && echo "wire ok" \
     && HKV_STRESS_MS_BLOCKS=36 timeout -k 10 400 $P tests/test_gpu_sighash.py -k multisig_block_stress \
       > ${O}_multisig.log 2>&1 && echo "multisig ok" \
+    && HKV_STRESS_MS_BLOCKS=24 HKV_STRESS_MS_WINDOW=256,64 timeout -k 10 400 $P tests/test_gpu_sighash.py \
+      -k multisig_block_stress > ${O}_multisig_rounds.log 2>&1 && echo "multisig rounds ok" \
     && HKV_STRESS_ROUNDS=400 timeout -k 10 200 $P tests/test_gpu_concurrency.py \
       > ${O}_concurrency.log 2>&1 && echo "concurrency ok"
   ;;
