@@ -58,6 +58,9 @@ def test_bad_arguments_rejected_without_device(lib):
     assert lib.hkv_verify(None, None, 0, 0, None) == -1
     assert lib.hkv_verify_device(None, 0, None, 0, 0, None, None) == -1
     assert lib.hkv_batch_alloc(None, 10, ctypes.byref(ctypes.c_void_p())) == -1
+    assert lib.hkv_debug_ms_window(None, 0, 64, 64) == -1
+    assert lib.hkv_debug_ms_scratch(None, 0, ctypes.byref(ctypes.c_size_t())) == -1
+    assert lib.hkv_device_fault(None, 0, ctypes.byref(ctypes.c_uint32())) == -1
 
 
 def test_kernel_code_object_is_gfx950():
