@@ -64,6 +64,11 @@ UNC_PERMILLE = 100
 CONFIG4_N = 1 << 24
 CONFIG4_SEED = 0x484B5635
 CONFIG4_INVALID_PERMILLE = 50
+# SHA-256 (first 128 bits) of configs[4]'s global verdict bitmap (16,777,216
+# records, the default seed / pool / invalid share, LIBSECP mode) as one GPU
+# computes it, with and without the RCCL all-gather (profiles/r06a/, r06f/):
+# SURVEY §8(e)'s check that the N-GPU bitmap is bit-identical to the 1-GPU one
+CONFIG4_BITMAP_SHA = "3d2b3fc0ad2eacaae04c9f12bc5c16e0"
 
 
 def cgroup_cpu_quota() -> dict:
@@ -1206,6 +1211,9 @@ def main() -> None:
             "force_collective": bool(args.force_collective and world == 1 and not share),
             "gather_vs_local_mismatches": gather_vs_local,
             "bitmap_sha256_128": bitmap_sha,
+            "bitmap_equals_1gpu": (bitmap_sha == CONFIG4_BITMAP_SHA)
+                                  if (config4 and n_total == CONFIG4_N and seed == CONFIG4_SEED and args.mode == 0)
+                                  else None,
             "launcher": ("bench.py spawn" if os.environ.get("HKV_BENCH_SPAWNED") else
                          "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or "GROUP_RANK" in os.environ else
                          "external" if world > 1 else "single process"),

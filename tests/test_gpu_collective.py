@@ -54,3 +54,5 @@ def test_rccl_all_gather_one_rank_equals_no_collective():
     assert plain["collective"] is None and plain["mismatches"] == 0
     assert plain["config"]["global_batch"] == rc["config"]["global_batch"] == 16777216
     assert plain["bitmap_sha256_128"] == rc["bitmap_sha256_128"]
+    # the constant the N > 1 lines are checked against (bench.CONFIG4_BITMAP_SHA)
+    assert rc["bitmap_equals_1gpu"] is True and plain["bitmap_equals_1gpu"] is True
