@@ -15,7 +15,9 @@
 --
 --   * config record in the style of NodeConfig (src/Haskoin/Node.hs:74-96);
 --   * an actor in the style of withChain (src/Haskoin/Node/Chain.hs:277-307):
---     a mailbox, a forever/receive loop under withAsync + link;
+--     a mailbox and a receive loop under withAsync + link, which coalesces
+--     mempool txs into batched GPU calls and never lets a verify failure
+--     reach link (re-submit, then haskoin-core's CPU verifyStdInput);
 --   * fed by the node's events: blocks and txs arrive as
 --     PeerEvent (PeerMessage p (MBlock b)) / (MTx t), which
 --     Haskoin.Node.peerEvents (src/Haskoin/Node.hs:151-174) drops into its
@@ -39,6 +41,7 @@ module Haskoin.Node.Verify
     withVerifyActor,
     verifyBlock,
     verifyTx,
+    verifyWithPolicy,
   )
 where
 
