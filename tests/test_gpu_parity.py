@@ -304,8 +304,9 @@ def test_config4_adversarial_1m_both_modes(torch, ver, coracle, openssl):
     r = R.x >= n, high-S) plus 5% special valids (re-encoded and hybrid keys,
     the r + n branch, edge u1 / u2, u1 = 0, msg32 >= n, ladder collisions).
     The GPU bitmap must equal, in both modes and on EVERY record, the
-    construction labels and the C restatement; a 262,144-record slice must
-    also equal OpenSSL's ECDSA_do_verify behind the semantic adapter."""
+    construction labels, the C restatement and OpenSSL's ECDSA_do_verify
+    behind the semantic adapter (round 6: every record, was a 262,144-record
+    slice)."""
     from hkv import adversarial
     n = 1 << 20
     d = gen_device(torch, ver, n, seed=0x484B5634)
@@ -321,10 +322,9 @@ def test_config4_adversarial_1m_both_modes(torch, ver, coracle, openssl):
         exp = oracle_batch(coracle, adv.tobytes(), mode, threads=th)
         mism = np.nonzero(got != exp)[0]
         assert mism.size == 0, (mode, "C oracle", mism[:10])
-        lo = 400_000
-        sl = slice(lo * 168, (lo + 262144) * 168)
-        ossl = openssl_batch(openssl, adv[sl].tobytes(), mode, threads=th)
-        assert (got[lo:lo + 262144] == ossl).all(), (mode, "openssl")
+        ossl = openssl_batch(openssl, adv.tobytes(), mode, threads=th)
+        mism = np.nonzero(got != ossl)[0]
+        assert mism.size == 0, (mode, "openssl", mism[:10])
 
 
 def gen_batch_dev(torch, ver, seed, index0, n, unc=100, pool=65536, inv=50):
@@ -539,12 +539,14 @@ def test_multi_device_failover_reshards(torch, ver):
 
 @pytest.mark.skipif(not os.environ.get("HKV_STRESS_RECORD_BATCHES"),
                     reason="stress run only (HKV_STRESS_RECORD_BATCHES=n)")
-def test_record_byte_mutation_stress(torch, ver, coracle):
+def test_record_byte_mutation_stress(torch, ver, coracle, openssl):
     """Opt-in stress (profiles/r05p/): n batches of 262,144 generated records
     with 30 % of them damaged at one random byte (any of the 168: msg32, r,
     s, the key's length byte, prefix or coordinates, the padding) to a random
     value; the verdicts of both modes, at the full-grid launch shape, equal
-    the C restatement's on every record."""
+    the C restatement's on every record, and (HKV_STRESS_OPENSSL=1) OpenSSL's
+    behind the semantic adapter too."""
+    use_ossl = os.environ.get("HKV_STRESS_OPENSSL") == "1"
     n = 262144
     for k in range(int(os.environ["HKV_STRESS_RECORD_BATCHES"])):
         d = gen_device(torch, ver, n, seed=0x53545200 + k, unc=200)
@@ -560,5 +562,9 @@ def test_record_byte_mutation_stress(torch, ver, coracle):
             got = ver.verify_records(flat, mode)
             mism = np.nonzero(got != exp)[0]
             assert mism.size == 0, (k, mode, mism[:10], [int(c) for c in cols[np.isin(rows, mism[:10])]])
-        print(f"record mutation stress: batch {k + 1}: {rows.size} damaged of {n}, accepts {int(got.sum())}",
-              flush=True)
+            if use_ossl:
+                ossl = openssl_batch(openssl, flat.tobytes(), mode, threads=host_threads())
+                mism = np.nonzero(got != ossl)[0]
+                assert mism.size == 0, (k, mode, "openssl", mism[:10])
+        print(f"record mutation stress: batch {k + 1}: {rows.size} damaged of {n}, accepts {int(got.sum())}"
+              + (" (C restatement and OpenSSL)" if use_ossl else ""), flush=True)

@@ -83,16 +83,19 @@ node)
     && echo "soak ok" && cat ${O}_soak.json
   ;;
 stress)
-  P="python -u -m pytest -s -x -v -m gpu --timeout 900 --timeout-method thread"
-  HKV_STRESS_RECORD_BATCHES=60 timeout -k 10 400 $P tests/test_gpu_parity.py -k record_byte_mutation_stress \
-      > ${O}_records.log 2>&1 && echo "records ok" \
-    && HKV_STRESS_SEEDS=300 timeout -k 10 400 $P tests/test_gpu_sighash.py -k wire_mutation_stress \
+  # STRESS_X scales every count and time limit (1: ~15 min; the records
+  # stress also checks OpenSSL when HKV_STRESS_OPENSSL=1)
+  X=${STRESS_X:-1}
+  P="python -u -m pytest -s -x -v -m gpu --timeout $((900 * X)) --timeout-method thread"
+  HKV_STRESS_RECORD_BATCHES=$((60 * X)) timeout -k 10 $((400 * X)) $P tests/test_gpu_parity.py \
+      -k record_byte_mutation_stress > ${O}_records.log 2>&1 && echo "records ok" \
+    && HKV_STRESS_SEEDS=$((300 * X)) timeout -k 10 $((400 * X)) $P tests/test_gpu_sighash.py -k wire_mutation_stress \
       > ${O}_wire.log 2>&1 && echo "wire ok" \
-    && HKV_STRESS_MS_BLOCKS=36 timeout -k 10 400 $P tests/test_gpu_sighash.py -k multisig_block_stress \
-      > ${O}_multisig.log 2>&1 && echo "multisig ok" \
-    && HKV_STRESS_MS_BLOCKS=24 HKV_STRESS_MS_WINDOW=256,64 timeout -k 10 400 $P tests/test_gpu_sighash.py \
-      -k multisig_block_stress > ${O}_multisig_rounds.log 2>&1 && echo "multisig rounds ok" \
-    && HKV_STRESS_ROUNDS=400 timeout -k 10 200 $P tests/test_gpu_concurrency.py \
+    && HKV_STRESS_MS_BLOCKS=$((36 * X)) timeout -k 10 $((400 * X)) $P tests/test_gpu_sighash.py \
+      -k multisig_block_stress > ${O}_multisig.log 2>&1 && echo "multisig ok" \
+    && HKV_STRESS_MS_BLOCKS=$((24 * X)) HKV_STRESS_MS_WINDOW=256,64 timeout -k 10 $((400 * X)) $P \
+      tests/test_gpu_sighash.py -k multisig_block_stress > ${O}_multisig_rounds.log 2>&1 && echo "multisig rounds ok" \
+    && HKV_STRESS_ROUNDS=$((400 * X)) timeout -k 10 $((200 * X)) $P tests/test_gpu_concurrency.py \
       > ${O}_concurrency.log 2>&1 && echo "concurrency ok"
   ;;
 *)
