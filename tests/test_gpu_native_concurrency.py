@@ -49,6 +49,12 @@ def test_overlapping_native_callers(blocks, variant, env, rounds):
                        env=dict(os.environ, **env))
     with open(os.path.join(OUT, f"native_concurrency{variant}.log"), "w") as f:
         f.write(r.stdout + "\n--- stderr ---\n" + r.stderr)
+    # a sanitizer runtime that cannot lay out its shadow memory on this host's
+    # address-space layout (e.g. TSan under high mmap randomisation) never
+    # reaches libhkv: the host, not the code under test
+    for fatal in ("ThreadSanitizer: unexpected memory mapping", "Shadow memory range interleaves"):
+        if fatal in r.stderr and not r.stdout.strip():
+            pytest.skip(f"{variant[1:]} runtime cannot start on this host: {fatal}")
     assert r.returncode == 0, r.stderr[-4000:]
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
     assert "WARNING: ThreadSanitizer" not in r.stderr
