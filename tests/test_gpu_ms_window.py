@@ -138,3 +138,31 @@ def test_multisig_free_chunk_within_budget(torch):
         b = ctypes.c_size_t()
         assert v.lib.hkv_debug_ms_scratch(v.ctx, 0, ctypes.byref(b)) == 0
         assert 0 < b.value <= BUDGET
+
+
+@pytest.mark.timeout(900)
+def test_two_chunks_with_multisig_on_both_sides(torch, ver, coracle):
+    """A batch past one 131,072-input chunk with multisig inputs in both
+    chunks (6,000 multisig inputs, 126,000 single-signature inputs, 6,000
+    more multisig inputs: the chunk boundary falls among the single-signature
+    inputs, so each chunk holds multisig inputs and the second chunk's jobs
+    start mid-batch): each chunk runs its own scan, windows and tail; verdicts
+    of the host form and of the device form with a status word equal the
+    oracle's, with no fault."""
+    import hkv
+    from hkv import blockgen
+    from test_gpu_sighash import _device_verify_std
+    mt1, mi1 = blockgen.make_multisig_block(ver, torch, n_tx=6000, seed=0x484B5647)
+    st_, si = blockgen.make_block(ver, torch, n_tx=76000, seed=0x484B5648, inputs_per_tx=(1, 2, 2, 2))
+    mt2, mi2 = blockgen.make_multisig_block(ver, torch, n_tx=6000, seed=0x484B5649)
+    txs = mt1 + st_ + mt2
+    o1, o2 = len(mt1), len(mt1) + len(st_)
+    si = si[:126000]
+    inputs = list(mi1) + [(t + o1, i, p, v) for (t, i, p, v) in si] + [(t + o2, i, p, v) for (t, i, p, v) in mi2]
+    assert len(si) == 126000 and len(inputs) == 138000 and len(mi1) + len(si) > 131072 > len(mi1)
+    want = batched_oracle(coracle, txs, inputs)
+    assert 0 < sum(not w for w in want) < 2000
+    assert hkv.verify_std_inputs(ver, txs, inputs) == want
+    got, st = _device_verify_std(torch, ver, txs, inputs, None, status=True)
+    assert st == 0 and got == want
+    assert ver.device_fault(0) == 0
