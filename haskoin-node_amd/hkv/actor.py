@@ -19,9 +19,11 @@ a mailbox drained by one loop.
   ``retries`` times, then handed to ``fallback`` — in the Haskell actor,
   haskoin-core's own per-input ``verifyStdInput``, the CPU path the drop-in
   replaces; this package has no CPU verifier of its own, so the caller
-  supplies it. With no fallback the batch's messages get ``VerifyFailed``.
-  Nothing is raised into the loop: a verify failure never stops the actor
-  (the Haskell actor runs under ``link``).
+  supplies it. With no fallback, or a fallback that raises, the batch's
+  messages get ``VerifyFailed``. Nothing is raised into the loop: a verify
+  failure never stops the actor (the Haskell actor runs under ``link``). A
+  bug in the loop itself (e.g. ``publish`` raising) ends it; ``stop`` re-raises
+  it and later posts raise at once instead of queueing unanswered.
 """
 from __future__ import annotations
 
@@ -122,10 +124,15 @@ class VerifyActor:
 
     # -- the mailbox ------------------------------------------------------------
     def verify_tx(self, key, tx: bytes, inputs: Sequence[Tuple[int, bytes, int]]) -> None:
-        self._q.put(_Tx(key, tx, list(inputs)))
+        self._post(_Tx(key, tx, list(inputs)))
 
     def verify_block(self, key, txs: Sequence[bytes], inputs: Sequence[Tuple[int, int, bytes, int]]) -> None:
-        self._q.put(_Block(key, list(txs), list(inputs)))
+        self._post(_Block(key, list(txs), list(inputs)))
+
+    def _post(self, msg) -> None:
+        if self._crash is not None:
+            raise RuntimeError("verify actor stopped on an error") from self._crash
+        self._q.put(msg)
 
     def start(self) -> "VerifyActor":
         if self._thread is None:
@@ -190,7 +197,17 @@ class VerifyActor:
                 self.stats.errors.append(err)
         if self.cfg.fallback is not None:
             self.stats.fallback_calls += 1
-            return [bool(x) for x in self.cfg.fallback(txs, inputs, self.cfg.forkid)], None
+            try:
+                ok = [bool(x) for x in self.cfg.fallback(txs, inputs, self.cfg.forkid)]
+            except Exception as e:  # the CPU path failed too: the batch is unverified
+                err = f"{err}; fallback: {e!r}"
+                self.stats.errors.append(err)
+                return None, err
+            if len(ok) != len(inputs):
+                err = f"{err}; fallback returned {len(ok)} verdicts for {len(inputs)} inputs"
+                self.stats.errors.append(err)
+                return None, err
+            return ok, None
         return None, err
 
     def _handle_block(self, m: _Block) -> None:

@@ -143,3 +143,38 @@ def test_no_fallback_publishes_failures_and_keeps_running(monkeypatch):
 def test_bad_config_rejected():
     with pytest.raises(ValueError):
         VerifyActor(None, print, VerifyActorConfig(max_inputs=0))
+
+
+def test_failing_fallback_publishes_failures_and_keeps_running(monkeypatch):
+    """A fallback that raises (or answers the wrong number of verdicts) leaves
+    the batch unverified: VerifyFailed for its messages, and the actor goes on
+    with the next ones."""
+    ev = tx_events(12)
+    calls = []
+
+    def fallback(txs, inputs, forkid):
+        calls.append(len(inputs))
+        if len(calls) == 1:
+            raise OSError("cpu path down")
+        return [True]  # wrong length
+    stub = StubGPU(fail={1, 2})
+    blk = ("blk2", [b"\x01"], [(0, 0, b"\x51", 1), (0, 1, b"\x51", 1)])
+    a, out = run(ev[:6] + [blk] + ev[6:], VerifyActorConfig(max_inputs=10**6, max_wait_s=1.0, retries=0,
+                                                          fallback=fallback), stub, monkeypatch)
+    assert all(isinstance(x, VerifyFailed) for x in out[:7]) and "cpu path down" in out[0].error
+    assert "verdicts" in out[6].error
+    assert out[7:] == expected(ev[6:]) and a.stats.fallback_calls == 2
+
+
+def test_posting_to_a_crashed_actor_raises(monkeypatch):
+    monkeypatch.setattr(actor, "verify_std_inputs", StubGPU())
+
+    def publish(_):
+        raise KeyError("subscriber bug")
+    a = VerifyActor(None, publish, VerifyActorConfig(max_wait_s=0.01)).start()
+    a.verify_tx("a", b"\x01abc", [(0, b"\x51", 1)])
+    a._thread.join(10)
+    with pytest.raises(RuntimeError):
+        a.verify_tx("b", b"\x02abc", [(0, b"\x51", 1)])
+    with pytest.raises(KeyError):
+        a.stop()
