@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import secp256k1_oracle as o
-from conftest import host_threads, openssl_batch, oracle_batch
+from conftest import fast_batch, host_threads, openssl_batch, oracle_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -355,16 +355,23 @@ def test_gen_batch_matches_c_restatement(torch, ver, coracle):
     assert (d.cpu().numpy() == plain).all() and adversarial.unpack_bits(lab, 4096).all()
 
 
-def test_config5_ibd_16m_sharded_bitmap(torch, ver, coracle):
+@pytest.mark.timeout(1500)
+def test_config5_ibd_16m_sharded_bitmap(torch, ver, coracle, secpfast):
     """BASELINE configs[4] exactly as bench.py runs it at N = 8, on one GPU:
     16,777,216 records (seed 0x484B5635, 5% invalid), each of the 8 shards
     (hkv/shard.py) GENERATED on its own with index0 = lo — as each rank does —
     and byte-equal to the same slice of the one-launch batch; the shards'
     verdict words assembled as the all-gather does equal the single-launch
     bitmap and the construction labels bit for bit; a sample of every shard
-    equals the C restatement's verdicts."""
+    equals the C restatement's verdicts: 65,536 records per shard, and EVERY
+    record of every shard, in both modes, equals the libsecp256k1-class
+    restatement (oracle/secp_fast.c) — north_star's "zero verdict mismatches
+    on 16M mixed valid/invalid signatures" against a checker rather than the
+    construction labels (~70 s on the GPU box's 16 host threads,
+    profiles/r06n/; HKV_FULL_16M=0 keeps only a 2,048-record sample)."""
     from hkv import adversarial
     from hkv.shard import assemble_bitmap, shard_bounds, words_per_rank
+    full_check = os.environ.get("HKV_FULL_16M", "1") not in ("", "0")
     n, world, seed = 1 << 24, 8, 0x484B5635
     d, lab = gen_batch_dev(torch, ver, seed, 0, n)
     labels = adversarial.unpack_bits(lab, n)
@@ -379,8 +386,19 @@ def test_config5_ibd_16m_sharded_bitmap(torch, ver, coracle):
         assert (adversarial.unpack_bits(ls, hi - lo) == labels[lo:hi]).all()
         w = verify_dev_bits(torch, ver, ds, hi - lo, 0)
         gathered[r * wpr: r * wpr + w.size] = w
-        exp = oracle_batch(coracle, ds[:2048 * 168].cpu().numpy().tobytes(), 0, threads=host_threads())
-        assert (adversarial.unpack_bits(w, 2048) == exp).all(), r
+        k = 65536 if full_check else 2048
+        exp = oracle_batch(coracle, ds[:k * 168].cpu().numpy().tobytes(), 0, threads=host_threads())
+        assert (adversarial.unpack_bits(w, k) == exp).all(), r
+        if full_check:
+            host = ds.cpu().numpy()
+            for mode in (0, 1):
+                wm = w if mode == 0 else verify_dev_bits(torch, ver, ds, hi - lo, 1)
+                exp = fast_batch(secpfast, host, mode, threads=host_threads())
+                mism = np.nonzero(adversarial.unpack_bits(wm, hi - lo) != exp)[0]
+                assert mism.size == 0, (r, mode, "secp_fast", mism[:10])
+                print(f"shard {r} mode {mode}: {hi - lo} records equal to secp_fast, {int(exp.sum())} accepted",
+                      flush=True)
+            del host
         del ds
     full = assemble_bitmap(n, world, gathered, wpr)
     assert (full == whole).all()

@@ -21,32 +21,16 @@ import numpy as np
 import pytest
 
 import secp256k1_oracle as o
-from conftest import GOLDEN, ROOT, c_gen_batch, oracle_batch
+from conftest import GOLDEN, ROOT, c_gen_batch, fast_batch, oracle_batch
 from hkv import adversarial
 
-FAST_SO = os.path.join(ROOT, "oracle", "build", "libhkv_secpfast.so")
-
-
 @pytest.fixture(scope="module")
-def fast():
-    if not os.path.exists(FAST_SO):
-        import subprocess
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    lib = ctypes.CDLL(FAST_SO)
-    lib.hkvo_fast_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
-                                           ctypes.c_int]
+def fast(secpfast):
+    lib = secpfast
     lib.hkvo_fast_sc_inverse.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     lib.hkvo_fast_glv_split.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]
     return lib
-
-
-def fast_batch(lib, recs, mode, threads=8):
-    recs = np.ascontiguousarray(np.frombuffer(bytes(recs), dtype=np.uint8) if isinstance(recs, bytes) else recs)
-    n = len(recs) // 168
-    out = np.zeros(n, dtype=np.uint8)
-    lib.hkvo_fast_verify_batch(recs.ctypes.data, n, mode, out.ctypes.data, threads)
-    return out.astype(bool)
 
 
 @pytest.mark.parametrize("mode,key", [(0, "libsecp"), (1, "haskoin")])
