@@ -146,3 +146,19 @@ def test_cpu_baseline_reports_both_whole_host_extrapolations(coracle, monkeypatc
     assert list(r)[0] == "whole_host_smt_extrapolated"
     assert r["whole_host_smt_extrapolated"] == round(1e8 / wh["smt_extrapolated_value"], 1)
     assert r["target_met_whole_host"] == (r["whole_host_smt_extrapolated"] >= 50.0)
+
+
+def test_bench_checker_leg_counts_mismatches(coracle, secpfast):
+    """bench.py's mismatches_vs_checker leg: every record of the slice through
+    secp_fast, compared bit for bit with the slice of the gathered bitmap —
+    0 on the construction labels of a configs[4]-style slice, and a flipped
+    verdict is counted."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    recs, lab, _ = c_gen_batch(coracle, 0x484B5635, 777_000, 2000, 65536, 100, 50)
+    r = bench.checker_leg(recs, lab, 0)
+    assert r["checked"] == 2000 and r["mismatches"] == 0 and r["checker"] == "oracle/secp_fast.c"
+    bad = lab.copy()
+    bad[[3, 1999]] ^= True
+    assert bench.checker_leg(recs, bad, 0)["mismatches"] == 2

@@ -40,7 +40,8 @@ try:
     d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
     c0 = (d.get("config0") or {}).get("total_us")
     print(sys.argv[1], round(d["value"] / 1e6, 2), "M/s", d["ms_per_step"], "ms/step", "frac",
-          d["roofline"]["frac"], "mism", d["mismatches"], "config0_us", c0, "collective", d.get("collective"))
+          d["roofline"]["frac"], "mism", d["mismatches"], "vs_checker", (d.get("mismatches_vs_checker") or {}).get("mismatches"),
+          "config0_us", c0, "collective", d.get("collective"))
 except Exception as e:
     print(sys.argv[1], "unreadable", e)
 PY
