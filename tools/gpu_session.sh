@@ -3,6 +3,10 @@
 # gpurun_out/<TAG>_*. Every GPU step runs under its own time limit and the
 # steps are chained, so the first failure ends the session.
 #
+#   tools/gpu_session.sh suite TAG     the GPU suite and smoke (evidence's first half)
+#   tools/gpu_session.sh benches TAG   evidence's second half (from the benches on);
+#                                      the two halves fit gpurun's 1,200-s limit
+#                                      where the whole session may not
 #   tools/gpu_session.sh evidence TAG  the GPU suite, smoke, the default bench
 #                                      twice (cpu_baseline agreement), the
 #                                      --share-device two-rank spawn, the
@@ -27,7 +31,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-MODE=${1:?mode: evidence | node | stress}
+MODE=${1:?mode: evidence | suite | benches | node | stress}
 TAG=${2:-$MODE}
 O=gpurun_out/${TAG}
 S="--no-cpu-baseline --no-block-mix --no-config0 --no-adversarial --no-headers --no-merkle --no-host-path --no-inproc"
@@ -48,12 +52,14 @@ PY
   done
 }
 
-case "$MODE" in
-evidence)
-  timeout -k 10 1200 python -u -m pytest -x -v -m gpu --timeout 800 --timeout-method thread tests \
+suite_half() {
+  timeout -k 10 1100 python -u -m pytest -x -v -m gpu --timeout 800 --timeout-method thread tests \
       > ${O}_pytest_gpu.log 2>&1 && echo "pytest ok" && tail -1 ${O}_pytest_gpu.log \
-    && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 && echo "smoke ok" \
-    && timeout -k 10 600 python bench.py > ${O}_bench1.log 2>&1 && echo "bench1 ok" \
+    && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 && echo "smoke ok"
+}
+
+benches_half() {
+  timeout -k 10 600 python bench.py > ${O}_bench1.log 2>&1 && echo "bench1 ok" \
     && timeout -k 10 600 python bench.py > ${O}_bench2.log 2>&1 && echo "bench2 ok" \
     && timeout -k 10 300 python bench.py --gpus 2 --share-device --config4-n 2097152 --steps 5 --warmup 1 \
          > ${O}_spawn2.log 2>&1 && echo "spawn2 ok" \
@@ -66,6 +72,17 @@ evidence)
          echo "--gpus 2 on the 1-GPU lease: rc=$rc (want 2)"; [ $rc -eq 2 ]; } \
     && summary ${O}_bench1.log ${O}_bench2.log ${O}_rccl1.log ${O}_torchrun_rccl1.log \
     && bash tools/profile_round.sh $TAG && echo "profile ok"
+}
+
+case "$MODE" in
+evidence)
+  suite_half && benches_half
+  ;;
+suite)
+  suite_half
+  ;;
+benches)
+  benches_half
   ;;
 node)
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_${TAG}_iso -o iso \
