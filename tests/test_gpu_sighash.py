@@ -976,12 +976,15 @@ def _wire_mutation_batch(torch, ver, coracle, seed, n_mut=1500):
 
 @pytest.mark.skipif(not os.environ.get("HKV_STRESS_SEEDS"), reason="stress run only (HKV_STRESS_SEEDS=n)")
 def test_block_kernel_wire_mutation_stress(torch, ver, coracle):
-    """The mutation batch above over HKV_STRESS_SEEDS further seeds (a stress
-    run outside the suite: profiles/r05o/)."""
+    """The mutation batch above over HKV_STRESS_SEEDS further seeds, from
+    seed index HKV_STRESS_SEED0 (default 0; a stress run outside the suite:
+    profiles/r05o/, r06h/, r06q/)."""
+    k0 = int(os.environ.get("HKV_STRESS_SEED0", "0"))
     for k in range(int(os.environ["HKV_STRESS_SEEDS"])):
-        _wire_mutation_batch(torch, ver, coracle, 0x5EED0000 + k)
+        _wire_mutation_batch(torch, ver, coracle, 0x5EED0000 + k0 + k)
         if k % 20 == 19:
-            print(f"wire mutation stress: {k + 1} batches ({(k + 1) * 1500} mutants) match", flush=True)
+            print(f"wire mutation stress: {k + 1} batches ({(k + 1) * 1500} mutants, seeds from {k0}) match",
+                  flush=True)
 
 
 @pytest.mark.skipif(not os.environ.get("HKV_STRESS_MS_BLOCKS"), reason="stress run only (HKV_STRESS_MS_BLOCKS=n)")
