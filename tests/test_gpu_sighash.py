@@ -996,13 +996,15 @@ def test_multisig_block_stress(torch, ver, coracle):
     (and every fifth batch the host form) equal the oracle's on every input,
     and no call reports a tail fault. HKV_STRESS_MS_WINDOW=c,k runs every
     batch with the tail's record windows forced to c candidate / k key-check
-    records (hkv_debug_ms_window: many rounds per batch)."""
+    records (hkv_debug_ms_window: many rounds per batch); HKV_STRESS_SEED0
+    starts at a later batch seed."""
     import hkv
+    k0 = int(os.environ.get("HKV_STRESS_SEED0", "0"))
     win = os.environ.get("HKV_STRESS_MS_WINDOW")
     if win:
         c, kk = (int(x) for x in win.split(","))
         assert ver.lib.hkv_debug_ms_window(ver.ctx, 0, c, kk) == 0
-    for k in range(int(os.environ["HKV_STRESS_MS_BLOCKS"])):
+    for k in range(k0, k0 + int(os.environ["HKV_STRESS_MS_BLOCKS"])):
         forkid = None if k % 2 == 0 else 0
         raw, jobs, labels = _ms_block(random.Random(0x4D530000 + k), forkid)
         want = _ms_oracle(coracle, raw, jobs, forkid)
