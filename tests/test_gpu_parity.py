@@ -557,16 +557,19 @@ def test_multi_device_failover_reshards(torch, ver):
 
 @pytest.mark.skipif(not os.environ.get("HKV_STRESS_RECORD_BATCHES"),
                     reason="stress run only (HKV_STRESS_RECORD_BATCHES=n)")
-def test_record_byte_mutation_stress(torch, ver, coracle, openssl):
+def test_record_byte_mutation_stress(torch, ver, coracle, openssl, secpfast):
     """Opt-in stress (profiles/r05p/): n batches of 262,144 generated records
     with 30 % of them damaged at one random byte (any of the 168: msg32, r,
     s, the key's length byte, prefix or coordinates, the padding) to a random
     value; the verdicts of both modes, at the full-grid launch shape, equal
     the C restatement's on every record, and (HKV_STRESS_OPENSSL=1) OpenSSL's
-    behind the semantic adapter too."""
+    behind the semantic adapter too, and the libsecp256k1-class restatement
+    (oracle/secp_fast.c) always. HKV_STRESS_SEED0 starts at a later batch
+    seed."""
     use_ossl = os.environ.get("HKV_STRESS_OPENSSL") == "1"
     n = 262144
-    for k in range(int(os.environ["HKV_STRESS_RECORD_BATCHES"])):
+    k0 = int(os.environ.get("HKV_STRESS_SEED0", "0"))
+    for k in range(k0, k0 + int(os.environ["HKV_STRESS_RECORD_BATCHES"])):
         d = gen_device(torch, ver, n, seed=0x53545200 + k, unc=200)
         host = d.cpu().numpy().copy().reshape(-1, 168)
         rng = np.random.default_rng(0x5EED + k)
@@ -580,9 +583,12 @@ def test_record_byte_mutation_stress(torch, ver, coracle, openssl):
             got = ver.verify_records(flat, mode)
             mism = np.nonzero(got != exp)[0]
             assert mism.size == 0, (k, mode, mism[:10], [int(c) for c in cols[np.isin(rows, mism[:10])]])
+            mism = np.nonzero(got != fast_batch(secpfast, flat, mode, threads=host_threads()))[0]
+            assert mism.size == 0, (k, mode, "secp_fast", mism[:10])
             if use_ossl:
                 ossl = openssl_batch(openssl, flat.tobytes(), mode, threads=host_threads())
                 mism = np.nonzero(got != ossl)[0]
                 assert mism.size == 0, (k, mode, "openssl", mism[:10])
         print(f"record mutation stress: batch {k + 1}: {rows.size} damaged of {n}, accepts {int(got.sum())}"
-              + (" (C restatement and OpenSSL)" if use_ossl else ""), flush=True)
+              + (" (C restatement, secp_fast and OpenSSL)" if use_ossl else " (C restatement and secp_fast)"),
+              flush=True)
