@@ -514,19 +514,24 @@ def split_phases(v, torch, run, n_groups: int = 0) -> dict:
     return out
 
 
-def block_mix(v, torch, steps: int) -> dict:
+def block_mix(v, torch, steps: int, ibd_txs: int = 0) -> dict:
     """BASELINE configs[2]: a 2,000-tx P2PKH + P2WPKH block verified end to
     end on device from HBM-resident tx bytes; plus the same pipeline on a
     mempool-sized batch (9,000 txs, ~16,000 inputs: the pair kernel's range,
     4,097-32,768 inputs) and a 32-block batch (64,000 txs: the overlapped
-    full-grid path) for their throughput. Every generated input is
-    valid; `rejected` must be 0 (the per-input records are checked against the
-    oracle byte for byte in tests/test_gpu_sighash.py, not here)."""
+    full-grid path) for their throughput; --std-ibd N adds one N-tx batch
+    (e.g. 560,000 txs, ~1M inputs: an IBD-sized getBlocks list of blocks
+    through the verifyStdInput path, sighash on device). Every generated
+    input is valid; `rejected` must be 0 (the per-input records are checked
+    against the oracle byte for byte in tests/test_gpu_sighash.py, not here)."""
     from hkv import blockgen
     out = {}
     # a dedicated stream: torch's default stream is the null stream (pointer 0)
     bstream = torch.cuda.Stream()
-    for label, n_tx in (("block", 2000), ("pool16k", 9000), ("batch32", 64000)):
+    sizes = [("block", 2000), ("pool16k", 9000), ("batch32", 64000)]
+    if ibd_txs:
+        sizes.append(("ibd", ibd_txs))
+    for label, n_tx in sizes:
         txs, inputs = blockgen.make_block(v, torch, n_tx=n_tx, seed=blockgen.SEED + n_tx)
         db = blockgen.DeviceBlock(torch, txs, inputs)
         out[label], _ = _time_block(v, torch, db, bstream, max(5, steps // (1 if label == "block" else 4)))
@@ -1033,6 +1038,8 @@ def main() -> None:
                     help="test only: at WORLD_SIZE 1 still create the nccl (RCCL) group with device_id and run the "
                          "step's all-gather of the verdict words on the device, on the stream libhkv enqueued on "
                          "(the N > 1 collective path on a 1-GPU lease)")
+    ap.add_argument("--std-ibd", type=int, default=0, metavar="N_TX",
+                    help="block_mix also times one N_TX-tx verifyStdInput batch (e.g. 560000: ~1M inputs)")
     ap.add_argument("--no-checker", action="store_true",
                     help="skip re-verifying every record of the slice on the host with oracle/secp_fast.c "
                          "(mismatches_vs_checker; outside the timed region)")
@@ -1206,7 +1213,7 @@ def main() -> None:
             c0, c0_recs, c0_got, c0_txs, c0_inputs = config0_block(v, torch, args.steps)
             c0["records_vs_oracle"] = config0_records_check(c0_txs, c0_inputs, c0_recs)
         if single and not args.no_block_mix:
-            mix = block_mix(v, torch, args.steps)
+            mix = block_mix(v, torch, args.steps, args.std_ibd)
         if single and not args.no_host_path:
             hp = host_path(v, recs, n, args.steps)
         if single and not args.no_headers:

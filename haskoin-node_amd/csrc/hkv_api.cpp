@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -72,6 +73,7 @@ struct DevCtx {
   void* ms[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   size_t ms_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   uint32_t ms_win_cand = 0, ms_win_keys = 0;  // record-window overrides (hkv_debug_ms_window; 0 = default)
+  size_t std_chunk = 0;  // verify-std-inputs chunk past one resident grid (init_device; enqueue_verify_std_inputs)
   void* ms_ctr = nullptr;            // scan sums: [epoch & 1] this call's (its tail launch zeroes the other)
   // the tail's words: [0..7] and [8..15] the two work-queue slots (claim,
   // completed items; launch `tail_epoch` uses slot tail_epoch & 1 and zeroes
@@ -147,14 +149,22 @@ size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 #define HKV_SPLIT_DIV 8
 #endif
 
-// verify-std-inputs batches run in chunks of at most STD_CHUNK inputs. The
+// verify-std-inputs batches run in chunks (enqueue_verify_std_inputs). The
 // multisig verdict bits of a chunk are sized by the host bound (136 candidate
 // and 16 key-check records per input: 16-of-16), so the device never reports
 // a count the host must read first (the scan's 32-bit candidate sum cannot
 // wrap); the 168-B records themselves live in two windows capped at
 // MS_WIN_CAND + MS_WIN_KEYS records (~512 MiB), through
 // which the tail kernel runs the chunk's records in rounds
-constexpr size_t STD_CHUNK = 1u << 17;
+// A batch of at most one resident grid runs in half-grid chunks (131,072
+// inputs on an MI355X: the overlapped mid-size form, hash half beside the Q
+// chains); a larger batch in chunks of up to std_chunk inputs (default 2^20;
+// env HKV_STD_CHUNK at open, for tests) through the full-grid instance:
+// extraction, then the record verify at 4 waves per SIMD. (Round 6: 1,007,894
+// inputs in 128k chunks took 15.96 ms, 63 M inputs/s, profiles/r06y/.)
+#ifndef HKV_STD_CHUNK
+#define HKV_STD_CHUNK (1u << 20)
+#endif
 constexpr size_t MS_CAND_PER_INPUT = 136, MS_KEYS_PER_INPUT = 16;
 #ifndef HKV_MS_WIN_CAND
 #define HKV_MS_WIN_CAND 2752512u  // 43,008 x 64 candidate records (441 MiB)
@@ -342,6 +352,13 @@ int init_device(DevCtx& d, int device) {
   HKV_TRY(hkv::ecmult_max_blocks_per_cu(&per_cu), "occupancy query");
   if (per_cu < 1) per_cu = 1;
   d.grid_max = (uint32_t)(d.n_cu * per_cu);
+  // test hook: a smaller (or larger) chunk past one grid; a multiple of 64,
+  // at most 2^24 (the scan's 32-bit candidate sum: 136 per input)
+  d.std_chunk = HKV_STD_CHUNK;
+  if (const char* e = std::getenv("HKV_STD_CHUNK")) {
+    const unsigned long long c = std::strtoull(e, nullptr, 10) / 64 * 64;
+    if (c >= 64 && c <= (1ull << 24)) d.std_chunk = (size_t)c;
+  }
   const size_t lanes = (size_t)d.grid_max * hkv::WG;
   HKV_TRY(hipMalloc(&d.qs, lanes * hkv::QTAB_QUADS * 16), "hipMalloc(qtab scratch)");
   HKV_TRY(hkv::launch_gtable(d.gtab, d.stream), "gtable launch");
@@ -497,7 +514,7 @@ int enqueue_std_verify_split(DevCtx& d, const hkv_txs* dt, const hkv_input_job* 
   return HKV_OK;
 }
 
-// Full verifyStdInput over a chunk of at most STD_CHUNK jobs, verdict bit i
+// Full verifyStdInput over one chunk of jobs (enqueue_verify_std_inputs), verdict bit i
 // -> out_bits (device), all enqueued on st (nothing waits on the host).
 // Single-signature templates: one record per input (recs) through the verify
 // kernels — small batches in one fused launch (tx index, then the block or
@@ -670,8 +687,10 @@ int enqueue_std_rest(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, si
 
 int enqueue_verify_std_inputs(DevCtx& d, const hkv_txs* dt, const hkv_input_job* jobs, size_t n, int32_t forkid,
                               void* recs, uint32_t* out_bits, hipStream_t st) {
-  for (size_t lo = 0; lo < n; lo += STD_CHUNK) {
-    const size_t cn = std::min(STD_CHUNK, n - lo);
+  const size_t grid_lanes = (size_t)d.grid_max * hkv::WG;
+  const size_t chunk = n > grid_lanes ? d.std_chunk : grid_lanes / 2;
+  for (size_t lo = 0; lo < n; lo += chunk) {
+    const size_t cn = std::min(chunk, n - lo);
     const int rc = enqueue_std_chunk(d, dt, jobs + lo, cn, forkid, static_cast<uint8_t*>(recs) + lo * hkv::REC_SIZE,
                                      out_bits + lo / 32, st);
     if (rc) return rc;

@@ -261,8 +261,9 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * the device: the tail, one launch after the verify on every path, reads it
  * and does nothing when it is 0), so a
  * caller may enqueue block k+1 while block k verifies, and hip_stream may be
- * gated on events recorded after the call. Batches run in chunks of 131,072
- * inputs. Multisig scratch per chunk: the verdict bits by the 16-of-16 bound
+ * gated on events recorded after the call. A batch of at most one resident
+ * grid (262,144 inputs on an MI355X) runs in chunks of half a grid (131,072),
+ * a larger one in chunks of up to 2^20 inputs. Multisig scratch per chunk: the verdict bits by the 16-of-16 bound
  * (136 candidate + 16 key-check bits per input) and the 168-B records in two
  * windows, the bound or at most 2,752,512 + 442,368 records (~512 MiB), which
  * the tail runs in rounds when a chunk's records exceed them: ~0.1 GB for a

@@ -166,3 +166,39 @@ def test_two_chunks_with_multisig_on_both_sides(torch, ver, coracle):
     got, st = _device_verify_std(torch, ver, txs, inputs, None, status=True)
     assert st == 0 and got == want
     assert ver.device_fault(0) == 0
+
+
+@pytest.mark.timeout(1200)
+def test_past_one_grid_full_grid_chunks(torch, ver, coracle):
+    """A batch past one resident grid (262,144 inputs) runs in chunks of up
+    to 2^20 inputs through the full-grid instance (extraction, then the record
+    verify at 4 waves per SIMD) instead of half-grid chunks: ~290,000 inputs,
+    multisig inputs at both ends, in one chunk through the host form and the
+    device form with a status word; and with HKV_STD_CHUNK=196608 (a fresh
+    context) as a full-grid chunk of 196,608 inputs followed by a half-grid
+    one — every verdict equal to the oracle's, no fault."""
+    import os
+    import hkv
+    from hkv import blockgen
+    from test_gpu_sighash import _device_verify_std
+    mt1, mi1 = blockgen.make_multisig_block(ver, torch, n_tx=3000, seed=0x484B564A)
+    st_, si = blockgen.make_block(ver, torch, n_tx=163000, seed=0x484B564B, inputs_per_tx=(1, 2, 2, 2))
+    mt2, mi2 = blockgen.make_multisig_block(ver, torch, n_tx=3000, seed=0x484B564C)
+    txs = mt1 + st_ + mt2
+    o1, o2 = len(mt1), len(mt1) + len(st_)
+    inputs = list(mi1) + [(t + o1, i, p, v) for (t, i, p, v) in si] + [(t + o2, i, p, v) for (t, i, p, v) in mi2]
+    assert len(inputs) > 262144 + 20000
+    want = batched_oracle(coracle, txs, inputs)
+    assert 0 < sum(not w for w in want) < 1000
+    assert hkv.verify_std_inputs(ver, txs, inputs) == want
+    got, st = _device_verify_std(torch, ver, txs, inputs, None, status=True)
+    assert st == 0 and got == want
+    assert ver.device_fault(0) == 0
+    os.environ["HKV_STD_CHUNK"] = "196608"
+    try:
+        with hkv.Verifier(hkv.VerifierConfig(device_ids=[0], flags=1)) as v2:
+            got, st = _device_verify_std(torch, v2, txs, inputs, None, status=True)
+            assert st == 0 and got == want
+            assert v2.device_fault(0) == 0
+    finally:
+        del os.environ["HKV_STD_CHUNK"]
