@@ -17,6 +17,7 @@
 #   tools/gpu_session.sh node TAG      the node's view: the isolated tip-block
 #                                      call under a kernel trace, the native C ABI
 #                                      caller, configs[4] at the N > 1 shard sizes,
+#                                      an IBD-sized verifyStdInput batch (--std-ibd),
 #                                      a 120-s sustained 1M run
 #   tools/gpu_session.sh stress TAG    the opt-in stress tests (record / wire
 #                                      mutations, multisig blocks — also with the
@@ -96,6 +97,8 @@ node)
     && timeout -k 10 300 python bench.py --config4 --config4-n 2097152 --steps 10 --warmup 2 $S > ${O}_c4_2M.log 2>&1 \
     && timeout -k 10 300 python bench.py --config4 --config4-n 8388608 --steps 5 --warmup 1 $S > ${O}_c4_8M.log 2>&1 \
     && timeout -k 10 300 python bench.py --steps 10 --warmup 2 $S > ${O}_c1.log 2>&1 \
+    && timeout -k 10 400 python bench.py --steps 8 --warmup 1 --std-ibd 560000 --no-cpu-baseline --no-config0 \
+         --no-adversarial --no-headers --no-merkle --no-host-path --no-inproc --no-checker > ${O}_ibd.log 2>&1 \
     && summary ${O}_c4_2M.log ${O}_c4_8M.log ${O}_c1.log \
     && timeout -k 10 200 python3 tools/soak.py 120 15 > ${O}_soak.json 2> ${O}_soak.err \
     && echo "soak ok" && cat ${O}_soak.json
