@@ -263,7 +263,9 @@ int hkv_std_inputs_device(hkv_ctx* ctx, int dev, const hkv_txs* d_txs, const hkv
  * caller may enqueue block k+1 while block k verifies, and hip_stream may be
  * gated on events recorded after the call. A batch of at most one resident
  * grid (262,144 inputs on an MI355X) runs in chunks of half a grid (131,072),
- * a larger one in chunks of up to 2^20 inputs. Multisig scratch per chunk: the verdict bits by the 16-of-16 bound
+ * a larger one in chunks of up to 2^20 inputs (the environment variable
+ * HKV_STD_CHUNK, read at hkv_open, overrides the 2^20: a test hook). Multisig
+ * scratch per chunk: the verdict bits by the 16-of-16 bound
  * (136 candidate + 16 key-check bits per input) and the 168-B records in two
  * windows, the bound or at most 2,752,512 + 442,368 records (~512 MiB), which
  * the tail runs in rounds when a chunk's records exceed them: ~0.1 GB for a
